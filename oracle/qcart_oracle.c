@@ -1,0 +1,889 @@
+/*
+ * qcart_oracle.c — TEST INFRASTRUCTURE ONLY: CPU fp64 restatement of the reference stepper.
+ * See qcart_oracle.h for scope and PARITY STATUS (unpinned vs the reference binary; pinned by KATs).
+ *
+ * Every function cites the reference file:line it restates. Aliases:
+ *   HO/  = implementation codes/harmonic oscillator/
+ *   IHO/ = implementation codes/inverted harmonic oscillator/
+ *   QO/  = implementation codes/quartic oscillator/   (QO/simulation_quart.cpp == IQO copy)
+ *   IQO/ = implementation codes/inverted quartic oscillator/
+ * Third-party arithmetic restated: LAPACK zgbtf2/zgbtrs/ztbsv (via Intel MKL, version not pinned by
+ * the reference, HO/setupC.py:22) and MKL Inspector-Executor sparse mv descriptor semantics
+ * (SYMMETRIC/HERMITIAN + FILL_MODE_UPPER: only the upper triangle is read and mirrored).
+ */
+#include "qcart_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef struct { double re, im; } zc;
+
+/* per-thread scratch (avoids a large calloc per step in the OpenMP baseline) */
+static __thread zc* tls_buf = NULL;
+static __thread size_t tls_cap = 0;
+static zc* scratch_get(size_t n) {
+    if (n > tls_cap) {
+        free(tls_buf);
+        tls_buf = (zc*)malloc(n * sizeof(zc));
+        tls_cap = tls_buf ? n : 0;
+    }
+    return tls_buf;
+}
+
+static inline zc zadd(zc a, zc b) { zc r = {a.re + b.re, a.im + b.im}; return r; }
+static inline zc zsub(zc a, zc b) { zc r = {a.re - b.re, a.im - b.im}; return r; }
+static inline zc zmul(zc a, zc b) { zc r = {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; return r; }
+static inline zc zconj(zc a) { zc r = {a.re, -a.im}; return r; }
+static inline double cabs1(zc a) { return fabs(a.re) + fabs(a.im); }
+/* Fortran-style complex division (Smith's algorithm, as libgfortran) */
+static zc zdiv(zc a, zc b) {
+    zc r;
+    if (fabs(b.re) >= fabs(b.im)) {
+        double t = b.im / b.re, d = b.re + b.im * t;
+        r.re = (a.re + a.im * t) / d; r.im = (a.im - a.re * t) / d;
+    } else {
+        double t = b.re / b.im, d = b.re * t + b.im;
+        r.re = (a.re * t + a.im) / d; r.im = (a.im * t - a.re) / d;
+    }
+    return r;
+}
+
+struct qo_sys {
+    qo_params p;
+    int N, kl, fock, x0;
+    double w;      /* dot-product weight: 1 (Fock) or h (grid) */
+    double c;      /* force coupling: omega (Fock) or pi (grid) */
+    double* xl;    /* Fock: x_lower_diag[i] = X[i][i+1] = X[i+1][i]                  IHO/simulation_i.cpp:65-75 */
+    double* xg;    /* grid: x[i] = h*(i - x0)                                          QO/simulation_quart.cpp:48 */
+    double* hb;    /* H real band (2kl+1) x N: hb[(d+kl)*N + i] = H[i][i+d]            */
+    double* abim;  /* imag part of ab = I + i dt/2 H at F=0 per reference construction, (2kl+1) x N */
+    double* d2;    /* grid: Delta_2 dense band values (for ab construction), 2*4+1 */
+};
+
+struct qo_tab {
+    int N, kl, ldab, bwa;
+    zc* ab;        /* LAPACK AB (column-major), ldab = 2kl+kl+1, after zgbtf2 */
+    int32_t* ipiv; /* 0-based */
+    zc* A;         /* correction factor band (2 bwa + 1) x N: A[(d+bwa)*N + i] = A[i][i+d] */
+    int nswap;
+};
+
+int qo_dim(const qo_sys* s) { return s->N; }
+int qo_n_obs(const qo_sys* s) {
+    if (s->fock) return 5;
+    int m = s->p.moment_order;
+    return (2 + m + 1) * m / 2;
+}
+
+static double hget(const qo_sys* s, int i, int d) {
+    if (d < -s->kl || d > s->kl) return 0.;
+    int j = i + d;
+    if (i < 0 || i >= s->N || j < 0 || j >= s->N) return 0.;
+    return s->hb[(d + s->kl) * s->N + i];
+}
+static double xget(const qo_sys* s, int i, int j) {
+    if (i < 0 || j < 0 || i >= s->N || j >= s->N) return 0.;
+    if (s->fock) {
+        if (j == i + 1) return s->xl[i];
+        if (j == i - 1) return s->xl[j];
+        return 0.;
+    }
+    return (i == j) ? s->xg[i] : 0.;
+}
+
+/* Operator construction: Set_World ctors.
+ * Fock: IHO/simulation_i.cpp:45-151 (X: :65-75; H = -omega/2 (a+^2 + a^2): :119-124; ab bands :143-147)
+ *       HO/simulation.cpp:119-124 (H = omega (n+1/2), ab_center = H/2)
+ * Grid: QO/simulation_quart.cpp:46-200 (x :48, V :50, Delta_2 :71-93, ab :73-93, H :181-191) */
+qo_sys* qo_create(const qo_params* p) {
+    qo_sys* s = (qo_sys*)calloc(1, sizeof(qo_sys));
+    if (!s) return NULL;
+    s->p = *p;
+    s->fock = (p->family == QO_HO || p->family == QO_IHO);
+    if (s->fock) {
+        if (p->n_max < 4) { free(s); return NULL; }
+        s->N = p->n_max + 1;
+        s->kl = (p->family == QO_HO) ? 1 : 2;
+        s->w = 1.;
+        s->c = p->omega;
+    } else {
+        if (!(p->grid_size > 0.) || !(p->x_max > 0.)) { free(s); return NULL; }
+        s->x0 = (int)(p->x_max / p->grid_size + 0.5);
+        s->N = s->x0 * 2 + 1;
+        s->kl = 4;
+        s->w = p->grid_size;
+        s->c = M_PI;
+        if (p->moment_order < 1) s->p.moment_order = 5;
+    }
+    int N = s->N, kl = s->kl;
+    s->hb = (double*)calloc((size_t)(2 * kl + 1) * N, sizeof(double));
+    s->abim = (double*)calloc((size_t)(2 * kl + 1) * N, sizeof(double));
+    if (s->fock) {
+        s->xl = (double*)calloc(N, sizeof(double));
+        for (int i = 0; i < N - 1; i++) s->xl[i] = sqrt((double)(i + 1)) * sqrt(0.5);  /* IHO :66-72 */
+        s->xl[N - 1] = 0.;
+        const double om = p->omega;
+        if (p->family == QO_HO) {
+            for (int i = 0; i < N; i++) {
+                s->hb[(0 + kl) * N + i] = om * (0.5 + (double)i);                 /* HO :121 */
+                s->abim[(0 + kl) * N + i] = om * (0.5 + (double)i) * 0.5;         /* ab_center */
+            }
+        } else {
+            for (int i = 0; i + 2 < N; i++) {
+                /* (a a)[i][i+2] = sqrt(i+1)*sqrt(i+2); z_add alpha = -0.5*omega  IHO :119-124 */
+                double v = (-0.5 * om) * (sqrt((double)(i + 1)) * sqrt((double)(i + 2)));
+                s->hb[(2 + kl) * N + i] = v;          /* H[i][i+2] */
+                s->hb[(-2 + kl) * N + (i + 2)] = v;   /* H[i+2][i] */
+                s->abim[(2 + kl) * N + i] = v * 0.5;  /* ab_upper2 = diag*0.5     IHO :143-146 */
+                s->abim[(-2 + kl) * N + (i + 2)] = v * 0.5;
+            }
+        }
+    } else {
+        const double h = p->grid_size, lam = p->lambda_, m = p->mass;
+        s->xg = (double*)calloc(N, sizeof(double));
+        for (int i = 0; i < N; i++) s->xg[i] = h * ((double)(i - s->x0));
+        static const double num[5] = {-14350., 8064., -1008., 128., -9.};
+        double d2[5];
+        for (int d = 0; d < 5; d++) d2[d] = num[d] / 5040. / (h * h);   /* QO :71-93 */
+        for (int i = 0; i < N; i++) {
+            double x2 = s->xg[i] * s->xg[i];
+            double V = x2 * x2 * lam;                                    /* QO :49-50 */
+            /* H = p_hat_2/(2m) + V with p_hat_2 = -Delta_2              QO :182,191 */
+            s->hb[(0 + kl) * N + i] = (1. / (2. * m)) * (-d2[0]) + V;
+            s->abim[(0 + kl) * N + i] = (d2[0] * (-1.) / (2. * m) + V) * 0.5;  /* ab_center :73 */
+            for (int d = 1; d <= 4; d++) {
+                if (i + d < N) {
+                    double hv = (1. / (2. * m)) * (-d2[d]);
+                    s->hb[(d + kl) * N + i] = hv;
+                    s->hb[(-d + kl) * N + (i + d)] = hv;
+                    double av = 0.5 * d2[d] * (-1.) / (2. * m);          /* ab_upper/ab_lower :77-93 */
+                    s->abim[(d + kl) * N + i] = av;
+                    s->abim[(-d + kl) * N + (i + d)] = av;
+                }
+            }
+        }
+    }
+    return s;
+}
+
+void qo_destroy(qo_sys* s) {
+    if (!s) return;
+    free(s->xl); free(s->xg); free(s->hb); free(s->abim); free(s->d2);
+    free(s);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * reset_ab(change_t): IHO/simulation_i.cpp:227-277, HO/simulation.cpp:208-258, QO/simulation_quart.cpp:394-432
+ * ------------------------------------------------------------------------------------------- */
+
+/* real band product C = A*B, A half-width ka, B half-width kb (stored (2k+1) x N, [(d+k)*N+i] = M[i][i+d]) */
+static double* band_mul(int N, const double* A, int ka, const double* B, int kb, int* kc_out) {
+    int kc = ka + kb;
+    double* C = (double*)calloc((size_t)(2 * kc + 1) * N, sizeof(double));
+    for (int i = 0; i < N; i++)
+        for (int da = -ka; da <= ka; da++) {
+            int k = i + da;
+            if (k < 0 || k >= N) continue;
+            double a = A[(da + ka) * N + i];
+            if (a == 0.) continue;
+            for (int db = -kb; db <= kb; db++) {
+                int j = k + db;
+                if (j < 0 || j >= N) continue;
+                double b = B[(db + kb) * N + k];
+                C[(da + db + kc) * N + i] += a * b;
+            }
+        }
+    *kc_out = kc;
+    return C;
+}
+
+/* LAPACK zgbtf2 (unblocked band LU, partial pivoting by cabs1 = |re|+|im| as izamax), 0-based.
+ * AB column-major with leading dimension ldab = 2kl+ku+1; A(i,j) stored at AB[(kl+ku+i-j) + j*ldab]. */
+static int zgbtf2(int n, int kl, int ku, zc* ab, int ldab, int32_t* ipiv, int* nswap) {
+    const int kv = ku + kl;
+    int info = 0, ju = 0;
+    *nswap = 0;
+#define AB(r, c) ab[(r) + (size_t)(c) * ldab]
+    for (int j = ku + 1; j < (kv < n ? kv : n); j++)       /* fill-in columns KU+2..KV zeroed */
+        for (int i = kv - j; i < kl; i++) { AB(i, j).re = 0.; AB(i, j).im = 0.; }
+    for (int j = 0; j < n; j++) {
+        if (j + kv < n)
+            for (int i = 0; i < kl; i++) { AB(i, j + kv).re = 0.; AB(i, j + kv).im = 0.; }
+        int km = kl < (n - 1 - j) ? kl : (n - 1 - j);
+        int jp = 0;
+        double best = cabs1(AB(kv, j));
+        for (int t = 1; t <= km; t++) {
+            double v = cabs1(AB(kv + t, j));
+            if (v > best) { best = v; jp = t; }
+        }
+        ipiv[j] = j + jp;
+        if (AB(kv + jp, j).re != 0. || AB(kv + jp, j).im != 0.) {
+            int jn = j + ku + jp;
+            if (jn > n - 1) jn = n - 1;
+            if (jn > ju) ju = jn;
+            if (jp != 0) {
+                (*nswap)++;
+                for (int t = 0; t <= ju - j; t++) {   /* ZSWAP along the row (stride ldab-1) */
+                    zc tmp = AB(kv + jp - t, j + t);
+                    AB(kv + jp - t, j + t) = AB(kv - t, j + t);
+                    AB(kv - t, j + t) = tmp;
+                }
+            }
+            if (km > 0) {
+                zc one = {1., 0.};
+                zc rp = zdiv(one, AB(kv, j));
+                for (int t = 1; t <= km; t++) AB(kv + t, j) = zmul(rp, AB(kv + t, j));
+                for (int c = 1; c <= ju - j; c++) {   /* ZGERU rank-1 update in the band */
+                    zc y = AB(kv - c, j + c);
+                    if (y.re == 0. && y.im == 0.) continue;
+                    for (int t = 1; t <= km; t++) {
+                        zc prod = zmul(AB(kv + t, j), y);
+                        AB(kv + t - c, j + c) = zsub(AB(kv + t - c, j + c), prod);
+                    }
+                }
+            }
+        } else if (info == 0) {
+            info = j + 1;
+        }
+    }
+#undef AB
+    return info;
+}
+
+/* LAPACK zgbtrs ('N', nrhs=1) + ztbsv('U','N','N'). IHO/simulation_i.cpp:487, QO/simulation_quart.cpp:622 */
+static void zgbtrs1(int n, int kl, int ku, const zc* ab, int ldab, const int32_t* ipiv, zc* b) {
+    const int kd = ku + kl;   /* 0-based row of the diagonal */
+#define AB(r, c) ab[(r) + (size_t)(c) * ldab]
+    if (kl > 0) {
+        for (int j = 0; j < n - 1; j++) {
+            int lm = kl < (n - 1 - j) ? kl : (n - 1 - j);
+            int l = ipiv[j];
+            if (l != j) { zc t = b[l]; b[l] = b[j]; b[j] = t; }
+            zc bj = b[j];
+            for (int t = 1; t <= lm; t++) b[j + t] = zsub(b[j + t], zmul(AB(kd + t, j), bj));
+        }
+    }
+    const int k = kl + ku;
+    for (int j = n - 1; j >= 0; j--) {
+        if (b[j].re != 0. || b[j].im != 0.) {
+            b[j] = zdiv(b[j], AB(k, j));
+            zc temp = b[j];
+            int i0 = j - k > 0 ? j - k : 0;
+            for (int i = j - 1; i >= i0; i--) b[i] = zsub(b[i], zmul(temp, AB(k + i - j, j)));
+        }
+    }
+#undef AB
+}
+
+qo_tab* qo_make_tab(const qo_sys* s, double dt, double force, int* n_swaps) {
+    const int N = s->N, kl = s->kl, ku = kl, ldab = 2 * kl + ku + 1;
+    qo_tab* t = (qo_tab*)calloc(1, sizeof(qo_tab));
+    t->N = N; t->kl = kl; t->ldab = ldab; t->bwa = 5 * kl;
+    t->ab = (zc*)calloc((size_t)ldab * N, sizeof(zc));
+    t->ipiv = (int32_t*)calloc(N, sizeof(int32_t));
+    /* ab = I + i*(dt * abim_F): copy into rows kl.. of AB (ab_LU[kl][...] = ab, reset_ab :250) */
+#define ABr(r, c) t->ab[(r) + (size_t)(c) * ldab]
+    for (int i = 0; i < N; i++) {
+        for (int d = -kl; d <= kl; d++) {
+            int j = i + d;     /* A(i,j), row i col j */
+            if (j < 0 || j >= N) continue;
+            double im = 0.;
+            if (s->fock) {
+                if (d == 0 || d == 2 || d == -2) {
+                    if (s->p.family == QO_HO || d != 0) im = s->abim[(d + kl) * N + i] * dt;
+                }
+                if (d == 1 || d == -1) {
+                    int lo = i < j ? i : j;
+                    /* x_lower_diag_ab = -x*0.5*omega; dscal by dt*F   IHO :73-74, :230-235 */
+                    im = ((-s->xl[lo]) * 0.5 * s->p.omega) * (dt * force);
+                }
+            } else {
+                im = s->abim[(d + kl) * N + i] * dt;
+                if (d == 0) im += (-dt * force * 0.5 * M_PI) * s->xg[i];   /* QO :397-399 */
+            }
+            zc v = {(d == 0) ? 1. : 0., im};
+            ABr(kl + ku + i - j, j) = v;
+        }
+    }
+#undef ABr
+    int nsw = 0;
+    int info = zgbtf2(N, kl, ku, t->ab, ldab, t->ipiv, &nsw);
+    t->nswap = nsw;
+    if (n_swaps) *n_swaps = nsw;
+    if (info != 0) { qo_free_tab(t); return NULL; }
+
+    /* Hamiltonian_addup_factor = dt^3/12 H_F^2 - i dt^4/24 H_F^3 - dt^5/80 H_F^4 + i dt^6/360 H_F^5
+     * with H_F = H - c F X (z_add of x_hat * (-c F)): IHO :253-264, QO :414-425 */
+    double* HF = (double*)calloc((size_t)(2 * kl + 1) * N, sizeof(double));
+    for (int i = 0; i < N; i++)
+        for (int d = -kl; d <= kl; d++) {
+            int j = i + d;
+            if (j < 0 || j >= N) continue;
+            HF[(d + kl) * N + i] = (-s->c * force) * xget(s, i, j) + hget(s, i, d);
+        }
+    int k2, k3, k4, k5;
+    double* P2 = band_mul(N, HF, kl, HF, kl, &k2);
+    double* P3 = band_mul(N, P2, k2, HF, kl, &k3);
+    double* P4 = band_mul(N, P2, k2, P2, k2, &k4);
+    double* P5 = band_mul(N, P2, k2, P3, k3, &k5);
+    const int bw = 5 * kl;
+    t->A = (zc*)calloc((size_t)(2 * bw + 1) * N, sizeof(zc));
+    const double c2 = dt * dt * dt / 12., c3 = dt * dt * dt * dt / 24.;
+    const double c4 = dt * dt * dt * dt * dt / 80., c5 = dt * dt * dt * dt * dt * dt / 360.;
+    for (int i = 0; i < N; i++)
+        for (int d = -bw; d <= bw; d++) {
+            int j = i + d;
+            if (j < 0 || j >= N) continue;
+            double p2 = (d >= -k2 && d <= k2) ? P2[(d + k2) * N + i] : 0.;
+            double p3 = (d >= -k3 && d <= k3) ? P3[(d + k3) * N + i] : 0.;
+            double p4 = (d >= -k4 && d <= k4) ? P4[(d + k4) * N + i] : 0.;
+            double p5 = P5[(d + k5) * N + i];
+            zc v;
+            v.re = (-c4 * p4) + (c2 * p2);
+            v.im = (c5 * p5) + (-c3 * p3);
+            t->A[(d + bw) * N + i] = v;
+        }
+    free(HF); free(P2); free(P3); free(P4); free(P5);
+    return t;
+}
+
+void qo_free_tab(qo_tab* t) {
+    if (!t) return;
+    free(t->ab); free(t->ipiv); free(t->A); free(t);
+}
+int qo_tab_ldab(const qo_tab* t) { return t->ldab; }
+void qo_tab_export(const qo_tab* t, double* ab_lu, int32_t* ipiv, double* a_band) {
+    if (ab_lu) memcpy(ab_lu, t->ab, sizeof(zc) * (size_t)t->ldab * t->N);
+    if (ipiv) memcpy(ipiv, t->ipiv, sizeof(int32_t) * t->N);
+    if (a_band) memcpy(a_band, t->A, sizeof(zc) * (size_t)(2 * t->bwa + 1) * t->N);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Vector operators
+ * ------------------------------------------------------------------------------------------- */
+
+/* compute_x_hat_state(alpha, psi, beta, result): result = beta*result + alpha*X psi
+ * Fock: IHO/simulation_i.cpp:168-196 (beta==0 branch overwrites); grid: QO/simulation_quart.cpp:214-229 */
+static void x_apply(const qo_sys* s, double alpha, const zc* psi, double beta, zc* res) {
+    const int N = s->N;
+    if (s->fock) {
+        const double* xl = s->xl;
+        for (int i = 0; i < N; i++) {
+            double re, im;
+            if (i == 0) { re = psi[1].re * xl[0]; im = psi[1].im * xl[0]; }
+            else if (i == N - 1) { re = psi[N - 2].re * xl[N - 2]; im = psi[N - 2].im * xl[N - 2]; }
+            else {
+                re = psi[i + 1].re * xl[i] + psi[i - 1].re * xl[i - 1];
+                im = psi[i + 1].im * xl[i] + psi[i - 1].im * xl[i - 1];
+            }
+            if (beta == 0.) { res[i].re = alpha * re; res[i].im = alpha * im; }
+            else {
+                res[i].re *= beta; res[i].re += alpha * re;
+                res[i].im *= beta; res[i].im += alpha * im;
+            }
+        }
+    } else {
+        for (int i = 0; i < N; i++) {
+            if (beta == 0.) {
+                res[i].re = alpha * psi[i].re * s->xg[i];
+                res[i].im = alpha * psi[i].im * s->xg[i];
+            } else {
+                res[i].re *= beta; res[i].re += alpha * psi[i].re * s->xg[i];
+                res[i].im *= beta; res[i].im += alpha * psi[i].im * s->xg[i];
+            }
+        }
+    }
+}
+
+/* sum_j H[i][j] v[j] (real symmetric band; exact under any sparse descriptor) */
+static zc h_row(const qo_sys* s, const zc* v, int i) {
+    zc acc = {0., 0.};
+    for (int d = -s->kl; d <= s->kl; d++) {
+        int j = i + d;
+        if (j < 0 || j >= s->N) continue;
+        double h = s->hb[(d + s->kl) * s->N + i];
+        acc.re += h * v[j].re; acc.im += h * v[j].im;
+    }
+    return acc;
+}
+
+/* y = -i H v + (i c F) y : mkl_sparse_z_mv(NON_TRANSPOSE, {0,-1}, H, descr, v, {0, c F}, y)
+ * IHO/simulation_i.cpp:291,313; QO/simulation_quart.cpp:442,466 */
+static void h_mv_into(const qo_sys* s, const zc* v, double force, zc* y) {
+    const double cf = s->c * force;
+    for (int i = 0; i < s->N; i++) {
+        zc hv = h_row(s, v, i);
+        zc yo = y[i];
+        y[i].re = hv.im + (-cf * yo.im);
+        y[i].im = -hv.re + (cf * yo.re);
+    }
+}
+
+static double dotc_re(int n, const zc* a, const zc* b) {   /* Re cblas_zdotc */
+    double acc = 0.;
+    for (int i = 0; i < n; i++) acc += a[i].re * b[i].re + a[i].im * b[i].im;
+    return acc;
+}
+static double nrm2(int n, const zc* a) {
+    double acc = 0.;
+    for (int i = 0; i < n; i++) acc += a[i].re * a[i].re + a[i].im * a[i].im;
+    return sqrt(acc);
+}
+
+/* x_expct: IHO/simulation_i.cpp:197-203 (no weight), QO/simulation_quart.cpp:230-236 (*h) */
+double qo_x_expectation(const qo_sys* s, const double* psi_) {
+    const zc* psi = (const zc*)psi_;
+    zc* tmp = (zc*)malloc(sizeof(zc) * s->N);
+    x_apply(s, 1., psi, 0., tmp);
+    double r = dotc_re(s->N, psi, tmp) * s->w;
+    free(tmp);
+    return r;
+}
+static double x_expct_ws(const qo_sys* s, const zc* psi, zc* tmp) {
+    x_apply(s, 1., psi, 0., tmp);
+    return dotc_re(s->N, psi, tmp) * s->w;
+}
+
+/* D1: IHO/simulation_i.cpp:279-298, QO/simulation_quart.cpp:434-449 */
+static void D1(const qo_sys* s, const zc* st, double force, double gamma, zc* result, zc* rel,
+               double x_avg, zc* xs) {
+    const int N = s->N;
+    x_apply(s, 1., st, 0., xs);
+    for (int i = 0; i < N; i++) {                      /* relative_state = X st - <x> st */
+        rel[i].re = xs[i].re + (-x_avg) * st[i].re;
+        rel[i].im = xs[i].im + (-x_avg) * st[i].im;
+    }
+    h_mv_into(s, st, force, xs);                       /* xs = -i(H - cFX) st */
+    memcpy(result, xs, sizeof(zc) * N);
+    memcpy(xs, rel, sizeof(zc) * N);
+    x_apply(s, 1., rel, -x_avg, xs);                   /* (x-<x>)^2 st */
+    for (int i = 0; i < N; i++) {
+        result[i].re += (-gamma / 4.) * xs[i].re;
+        result[i].im += (-gamma / 4.) * xs[i].im;
+    }
+}
+
+/* D1ImRe: IHO/simulation_i.cpp:301-318, QO/simulation_quart.cpp:452-471 */
+static void D1ImRe(const qo_sys* s, const zc* st, double force, double gamma, zc* rIm, zc* rRe, zc* rel) {
+    const int N = s->N;
+    x_apply(s, 1., st, 0., rIm);
+    double x_avg = dotc_re(N, st, rIm) * s->w;         /* unnormalised mean */
+    for (int i = 0; i < N; i++) {
+        rel[i].re = rIm[i].re + (-x_avg) * st[i].re;
+        rel[i].im = rIm[i].im + (-x_avg) * st[i].im;
+    }
+    h_mv_into(s, st, force, rIm);
+    memcpy(rRe, rel, sizeof(zc) * N);
+    x_apply(s, -gamma / 4., rel, x_avg * gamma / 4., rRe);
+}
+
+/* D2: IHO/simulation_i.cpp:320-333, QO/simulation_quart.cpp:473-486 */
+static void D2(const qo_sys* s, const zc* st, double gamma, zc* rr, int precomputed) {
+    const int N = s->N;
+    if (!precomputed) {
+        x_apply(s, 1., st, 0., rr);
+        double x_avg = dotc_re(N, st, rr) * s->w;
+        for (int i = 0; i < N; i++) {
+            rr[i].re += (-x_avg) * st[i].re;
+            rr[i].im += (-x_avg) * st[i].im;
+        }
+    }
+    const double sc = sqrt(gamma / 2.);
+    for (int i = 0; i < N; i++) { rr[i].re *= sc; rr[i].im *= sc; }
+}
+
+/* term7 = A D1 under the reference's sparse descriptor (App. C H1):
+ *   IHO: HERMITIAN/UPPER (IHO/simulation_i.cpp:23,551)  -> triu(A) + triu(A,1)^H (stored complex diagonal kept)
+ *   HO, grid: SYMMETRIC/UPPER (HO/simulation.cpp:532, QO/simulation_quart.cpp:25,631) -> triu(A) + triu(A,1)^T
+ *   a_mode == 1: the full (intended) complex-symmetric A. */
+static void term7_apply(const qo_sys* s, const qo_tab* t, const zc* v, zc* y) {
+    const int N = s->N, bw = t->bwa;
+    const int herm = (s->p.family == QO_IHO) && (s->p.a_mode == 0);
+    const int full = (s->p.a_mode == 1);
+    for (int i = 0; i < N; i++) {
+        zc acc = {0., 0.};
+        for (int d = -bw; d <= bw; d++) {
+            int j = i + d;
+            if (j < 0 || j >= N) continue;
+            zc a;
+            if (full || d >= 0) a = t->A[(d + bw) * N + i];          /* A[i][j], upper or full */
+            else {
+                a = t->A[(-d + bw) * N + j];                          /* stored upper A[j][i] */
+                if (herm) a = zconj(a);
+            }
+            acc = zadd(acc, zmul(a, v[j]));
+        }
+        y[i] = acc;
+    }
+}
+
+/* simple_sum_up: IHO/simulation_i.cpp:546-563, QO/simulation_quart.cpp:626-643 */
+static void sum_up(const qo_sys* s, const qo_tab* t, double* st, double dt, double dW, double dZ,
+                   const double* D2s, const double* dIm, const double* D1Rp, const double* D1Rm,
+                   const double* D1s, const double* D2Yp, const double* D2Ym, const double* D2Pp,
+                   const double* D2Pm, zc* scratch) {
+    term7_apply(s, t, (const zc*)D1s, scratch);
+    const double* t7 = (const double*)scratch;
+    const double sdt = sqrt(dt);
+    for (int i = 0; i < 2 * s->N; i++) {
+        st[i] += D2s[i] * dW + 0.5 / sdt * dZ * (dIm[i] + D1Rp[i] - D1Rm[i]) +
+                 0.25 * dt * (D1Rp[i] + 2 * D1s[i] + D1Rm[i]) +
+                 0.25 / sdt * (dW * dW - dt) * (D2Yp[i] - D2Ym[i]) +
+                 0.5 / dt * (dW * dt - dZ) * (D2Yp[i] + D2Ym[i] - 2 * D2s[i]) +
+                 0.25 / dt * (dW * dW / 3 - dt) * dW * (D2Pp[i] - D2Pm[i] - D2Yp[i] + D2Ym[i])
+                 - 0.25 * sdt * dW * (dIm[i]) + t7[i];
+    }
+}
+
+/* check_boundary_error: IHO/simulation_i.cpp:422-426 (5 top levels > 2e-3), HO/simulation.cpp:403-407
+ * (> 1e-3), QO/simulation_quart.cpp:559-565 (6 points at either end > 5e-3) */
+int qo_boundary_fail(const qo_sys* s, const double* psi_) {
+    const zc* psi = (const zc*)psi_;
+    const int N = s->N;
+    if (s->fock) {
+        double thr = (s->p.family == QO_HO) ? 1.e-3 : 2.e-3;
+        return nrm2(5, psi + N - 5) > thr;
+    }
+    return (nrm2(6, psi + N - 6) > 5.e-3) || (nrm2(6, psi) > 5.e-3);
+}
+
+/* go_one_step: IHO/simulation_i.cpp:432-489, HO/simulation.cpp:413-470, QO/simulation_quart.cpp:569-624 */
+void qo_step(const qo_sys* s, const qo_tab* t, double* psi_, double dt, double force, double gamma,
+             const double r[2], double* q_out, double* xm_out, int* fail) {
+    const int N = s->N;
+    zc* psi = (zc*)psi_;
+    zc* buf = scratch_get((size_t)N * 16);
+    zc *D1s = buf, *D2s = buf + N, *D2drt = buf + 2 * N, *Yp = buf + 3 * N, *Ym = buf + 4 * N;
+    zc *D1Ip = buf + 5 * N, *D1Rp = buf + 6 * N, *D2Yp = buf + 7 * N, *D1Im = buf + 8 * N;
+    zc *D1Rm = buf + 9 * N, *D2Ym = buf + 10 * N, *D2Pp = buf + 11 * N, *D2Pm = buf + 12 * N;
+    zc *xs = buf + 13 * N, *scratch = buf + 14 * N;
+
+    const double dW = r[0] * sqrt(dt), dZ = sqrt(dt) * dt * 0.5 * (r[0] + r[1] / sqrt(3.));
+    const double x_mean = x_expct_ws(s, psi, buf + 15 * N);
+    const double q = x_mean + dW / sqrt(2. * gamma) / dt;
+    if (q_out) *q_out = q;
+    if (xm_out) *xm_out = x_mean;
+
+    D1(s, psi, force, gamma, D1s, D2s, x_mean, xs);
+    D2(s, psi, gamma, D2s, 1);
+    const double sdt = sqrt(dt);
+    for (int i = 0; i < N; i++) { D2drt[i].re = sdt * D2s[i].re; D2drt[i].im = sdt * D2s[i].im; }
+    for (int i = 0; i < N; i++) {
+        Yp[i].re = psi[i].re + dt * D1s[i].re;
+        Yp[i].im = psi[i].im + dt * D1s[i].im;
+    }
+    memcpy(Ym, Yp, sizeof(zc) * N);
+    for (int i = 0; i < N; i++) {
+        Yp[i].re += 1. * D2drt[i].re; Yp[i].im += 1. * D2drt[i].im;
+        Ym[i].re += -1. * D2drt[i].re; Ym[i].im += -1. * D2drt[i].im;
+    }
+    D1ImRe(s, Yp, force, gamma, D1Ip, D1Rp, D2Yp);
+    D1ImRe(s, Ym, force, gamma, D1Im, D1Rm, D2Ym);
+    D2(s, Yp, gamma, D2Yp, 1);
+    D2(s, Ym, gamma, D2Ym, 1);
+    for (int i = 0; i < N; i++) {             /* D1_Y_plusIm - D1_Y_minusIm (in place) */
+        D1Ip[i].re += -1. * D1Im[i].re; D1Ip[i].im += -1. * D1Im[i].im;
+    }
+    zc* Phim = Ym;                            /* Phi_- = Y_+ - sqrt(dt) D2(Y_+) */
+    memcpy(Phim, Yp, sizeof(zc) * N);
+    for (int i = 0; i < N; i++) { Phim[i].re += -sdt * D2Yp[i].re; Phim[i].im += -sdt * D2Yp[i].im; }
+    zc* Phip = Yp;                            /* Phi_+ = Y_+ + sqrt(dt) D2(Y_+) */
+    for (int i = 0; i < N; i++) { Phip[i].re += sdt * D2Yp[i].re; Phip[i].im += sdt * D2Yp[i].im; }
+    D2(s, Phip, gamma, D2Pp, 0);
+    D2(s, Phim, gamma, D2Pm, 0);
+
+    sum_up(s, t, psi_, dt, dW, dZ, (double*)D2s, (double*)D1Ip, (double*)D1Rp, (double*)D1Rm,
+           (double*)D1s, (double*)D2Yp, (double*)D2Ym, (double*)D2Pp, (double*)D2Pm, scratch);
+    zgbtrs1(N, t->kl, t->kl, t->ab, t->ldab, t->ipiv, psi);
+    /* normalize: IHO/simulation_i.cpp:216-220 ; QO/simulation_quart.cpp:259-263 */
+    double nrm = nrm2(N, psi);
+    double scale = s->fock ? 1. / nrm : 1. / nrm / sqrt(s->p.grid_size);
+    for (int i = 0; i < N; i++) { psi[i].re *= scale; psi[i].im *= scale; }
+    if (fail) *fail = qo_boundary_fail(s, psi_);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Observations
+ * ------------------------------------------------------------------------------------------- */
+
+/* Fock 'xp' observation: IHO/main_parallel.py:129-131 with operators of adjust_n_max :53-79
+ * (x_hat = sqrt(1/2)(a+ + a), p_hat = i sqrt(1/2)(a+ - a), x_hat_2 = x.x, p_hat_2 = Re(p.p),
+ *  xp_px_hat = x.p + p.x, all truncated scipy products). */
+static void fock_moments(const qo_sys* s, const zc* psi, double* out) {
+    const int N = s->N;
+    const double sq = sqrt(0.5);
+    /* P band: P[i+1][i] = i sq sqrt(i+1), P[i][i+1] = -i sq sqrt(i+1) */
+    double* pv = (double*)calloc(N, sizeof(double));
+    for (int i = 0; i < N - 1; i++) pv[i] = sq * sqrt((double)(i + 1));
+    zc* Xp = (zc*)calloc(N, sizeof(zc));
+    zc* Pp = (zc*)calloc(N, sizeof(zc));
+    for (int i = 0; i < N; i++) {
+        zc xa = {0., 0.}, pa = {0., 0.};
+        if (i + 1 < N) {
+            xa.re += s->xl[i] * psi[i + 1].re; xa.im += s->xl[i] * psi[i + 1].im;
+            zc c = {0., -pv[i]}; pa = zadd(pa, zmul(c, psi[i + 1]));
+        }
+        if (i >= 1) {
+            xa.re += s->xl[i - 1] * psi[i - 1].re; xa.im += s->xl[i - 1] * psi[i - 1].im;
+            zc c = {0., pv[i - 1]}; pa = zadd(pa, zmul(c, psi[i - 1]));
+        }
+        Xp[i] = xa; Pp[i] = pa;
+    }
+    double xe = dotc_re(N, psi, Xp), pe = dotc_re(N, psi, Pp);
+    /* x.x, Re(p.p), x.p + p.x applied as explicit banded products (scipy semantics) */
+    double x2 = 0., p2 = 0., xppx = 0.;
+    for (int i = 0; i < N; i++) {
+        zc a2 = {0., 0.}, b2 = {0., 0.}, c2 = {0., 0.};
+        for (int d = -2; d <= 2; d++) {
+            int j = i + d;
+            if (j < 0 || j >= N) continue;
+            double xx = 0., pp = 0.;
+            zc xp = {0., 0.};
+            for (int k = i - 1; k <= i + 1; k += 2) {
+                if (k < 0 || k >= N) continue;
+                if (k != j - 1 && k != j + 1) continue;
+                double xik = xget(s, i, k), xkj = xget(s, k, j);
+                zc pik = {0., (k == i + 1) ? -pv[i] : pv[k]};
+                zc pkj = {0., (j == k + 1) ? -pv[k] : pv[j]};
+                xx += xik * xkj;
+                pp += zmul(pik, pkj).re;
+                zc t1 = {xik * pkj.re, xik * pkj.im};
+                zc t2 = {pik.re * xkj, pik.im * xkj};
+                xp = zadd(xp, zadd(t1, t2));
+            }
+            a2.re += xx * psi[j].re; a2.im += xx * psi[j].im;
+            b2.re += pp * psi[j].re; b2.im += pp * psi[j].im;
+            c2 = zadd(c2, zmul(xp, psi[j]));
+        }
+        x2 += psi[i].re * a2.re + psi[i].im * a2.im;
+        p2 += psi[i].re * b2.re + psi[i].im * b2.im;
+        xppx += psi[i].re * c2.re + psi[i].im * c2.im;
+    }
+    out[0] = xe; out[1] = pe;
+    out[2] = x2 - xe * xe;
+    out[3] = p2 - pe * pe;
+    out[4] = xppx / 2 - xe * pe;
+    free(pv); free(Xp); free(Pp);
+}
+
+/* grid p_hat under the HERMITIAN/UPPER descriptor with the reference's truncated Delta_1 loops
+ * (QO/simulation_quart.cpp:59-70, :239, :285): upper entry (r, r+d) exists iff r <= x_n-1-2d. */
+static void grid_p_apply(const qo_sys* s, const zc* v, double pbar, zc* out) {
+    static const double sd[5] = {0., 672., -168., 32., -3.};
+    const int N = s->N;
+    const double h = s->p.grid_size;
+    for (int r = 0; r < N; r++) {
+        zc acc = {0., 0.};
+        for (int d = 1; d <= 4; d++) {
+            double dl = sd[d] / 840. / h;   /* Delta_1(r, r+d) */
+            if (r + d < N && r <= N - 1 - 2 * d) {
+                zc c = {0., -dl}; acc = zadd(acc, zmul(c, v[r + d]));    /* -i Delta_1 */
+            }
+            if (r - d >= 0 && r <= N - 1 - d) {
+                zc c = {0., dl}; acc = zadd(acc, zmul(c, v[r - d]));     /* conj mirror */
+            }
+        }
+        out[r].re = acc.re - pbar * v[r].re;
+        out[r].im = acc.im - pbar * v[r].im;
+    }
+}
+
+/* compute_statistics: QO/simulation_quart.cpp:326-362 */
+static void grid_moments(const qo_sys* s, const zc* psi, double* data) {
+    const int N = s->N, m = s->p.moment_order;
+    const double h = s->p.grid_size;
+    zc* tmp = (zc*)calloc((size_t)(m + 1) * N, sizeof(zc));
+    double* xr = (double*)malloc(sizeof(double) * N);
+    data[0] = qo_x_expectation(s, (const double*)psi);
+    grid_p_apply(s, psi, 0., tmp);
+    data[1] = dotc_re(N, psi, tmp) * h;                                     /* p_expct :237-243 */
+    for (int i = 0; i < N; i++) xr[i] = s->xg[i] - data[0];
+    for (int i = 0; i < N; i++) { tmp[i].re = psi[i].re * xr[i]; tmp[i].im = psi[i].im * xr[i]; }
+    grid_p_apply(s, psi, data[1], tmp + N);
+    for (int k = 2; k <= m; k++) grid_p_apply(s, tmp + (size_t)(k - 1) * N, data[1], tmp + (size_t)k * N);
+    int di = 2;
+    for (int j = 2; j <= m; j++) {
+        for (int i = 0; i < j; i++) {
+            zc* v = tmp + (size_t)i * N;
+            for (int r = 0; r < N; r++) { v[r].re *= xr[r]; v[r].im *= xr[r]; }
+        }
+        for (int i = 0; i < j + 1; i++) data[di++] = dotc_re(N, psi, tmp + (size_t)i * N) * h;
+    }
+    free(tmp); free(xr);
+}
+
+void qo_moments(const qo_sys* s, const double* psi, double* out) {
+    if (s->fock) fock_moments(s, (const zc*)psi, out);
+    else grid_moments(s, (const zc*)psi, out);
+}
+
+/* calculate_outside_probability: IQO/main_parallel.py:78-81 (window [c-w, c+w), w = round(xth/h)) */
+double qo_outside_prob(const qo_sys* s, const double* psi_, double xth) {
+    const zc* psi = (const zc*)psi_;
+    const int c = s->N / 2;
+    const int w = (int)nearbyint(xth / s->p.grid_size);   /* Python round(): ties to even */
+    double acc = 0.;
+    int lo = c - w, hi = c + w;
+    if (lo < 0) lo = 0;
+    if (hi > s->N) hi = s->N;
+    for (int i = lo; i < hi; i++) acc += psi[i].re * psi[i].re + psi[i].im * psi[i].im;
+    return 1. - acc * s->p.grid_size;
+}
+
+double qo_energy(const qo_sys* s, const double* psi_) {   /* cal_energy, QO/main_parallel.py (H at F=0) */
+    const zc* psi = (const zc*)psi_;
+    double acc = 0.;
+    for (int i = 0; i < s->N; i++) {
+        zc hv = h_row(s, psi, i);
+        acc += psi[i].re * hv.re + psi[i].im * hv.im;
+    }
+    return acc * s->w;
+}
+double qo_phonon(const qo_sys* s, const double* psi_) {   /* phonon_number, HO/main_parallel.py:88-89 */
+    const zc* psi = (const zc*)psi_;
+    double acc = 0.;
+    for (int i = 0; i < s->N; i++) acc += (psi[i].re * psi[i].re + psi[i].im * psi[i].im) * (double)i;
+    return acc;
+}
+
+void qo_dense_h(const qo_sys* s, double* out) {
+    const int N = s->N;
+    memset(out, 0, sizeof(double) * (size_t)N * N);
+    for (int i = 0; i < N; i++)
+        for (int d = -s->kl; d <= s->kl; d++) {
+            int j = i + d;
+            if (j >= 0 && j < N) out[(size_t)i * N + j] = hget(s, i, d);
+        }
+}
+void qo_dense_x(const qo_sys* s, double* out) {
+    const int N = s->N;
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < N; j++) out[(size_t)i * N + j] = xget(s, i, j);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Counter-based noise (replaces MKL MT19937 + Box-Muller, App. C H3): spec in DESIGN.md §RNG
+ * ------------------------------------------------------------------------------------------- */
+static inline uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    *hi = (uint32_t)(p >> 32);
+    return (uint32_t)p;
+}
+void qo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; r++) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint32_t hi0, hi1;
+        uint32_t lo0 = mulhilo(0xD2511F53u, c0, &hi0);
+        uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, &hi1);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+static void normals_tag(uint64_t seed, uint64_t env, uint64_t ctr_lo, uint32_t tag, double r[2]) {
+    uint32_t ctr[4] = {(uint32_t)ctr_lo, (uint32_t)(ctr_lo >> 32), (uint32_t)env, tag};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    qo_philox4x32_10(ctr, key, o);
+    uint64_t a = (((uint64_t)o[0] << 32) | o[1]) >> 11;
+    uint64_t b = (((uint64_t)o[2] << 32) | o[3]) >> 11;
+    double u1 = ((double)a + 0.5) * 0x1.0p-53;
+    double u2 = ((double)b + 0.5) * 0x1.0p-53;
+    double rad = sqrt(-2. * log(u1));
+    double th = 2. * M_PI * u2;
+    r[0] = rad * cos(th);
+    r[1] = rad * sin(th);
+}
+void qo_normals(uint64_t seed, uint64_t env_id, uint64_t step, double r[2]) {
+    normals_tag(seed, env_id, step, 0u, r);
+}
+
+/* synthetic Fock psi0: complex Gaussian coefficients on levels n < levels, normalised */
+void qo_fock_random_state(const qo_sys* s, uint64_t seed, uint64_t env_id, int levels, double* psi_) {
+    zc* psi = (zc*)psi_;
+    memset(psi, 0, sizeof(zc) * s->N);
+    if (levels > s->N) levels = s->N;
+    double nn = 0.;
+    for (int k = 0; k < levels; k++) {
+        double r[2];
+        normals_tag(seed, env_id, (uint64_t)k, 1u, r);
+        psi[k].re = r[0]; psi[k].im = r[1];
+        nn += r[0] * r[0] + r[1] * r[1];
+    }
+    double sc = 1. / sqrt(nn);
+    for (int k = 0; k < levels; k++) { psi[k].re *= sc; psi[k].im *= sc; }
+}
+
+/* Gaussian_packet(wavelength, mean, std), IQO/main_parallel.py:75-76 (wavenumber = 1/wavelength) */
+void qo_gaussian_packet(const qo_sys* s, double k, double mean, double stdv, double* psi_) {
+    zc* psi = (zc*)psi_;
+    const double norm = sqrt(sqrt(2. * M_PI) * stdv);
+    for (int i = 0; i < s->N; i++) {
+        double x = s->xg ? s->xg[i] : 0.;
+        double ph = 2. * M_PI * (x - mean) * k;
+        double g = exp(-(x - mean) * (x - mean) / (4. * stdv * stdv)) / norm;
+        psi[i].re = cos(ph) * g;
+        psi[i].im = sin(ph) * g;
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Batched driver (cpu_baseline): one single-threaded env per thread, as the reference runs one
+ * MKL-sequential env per actor process (IHO/main_parallel.py:345-359, HO/setupC.py:44).
+ * ------------------------------------------------------------------------------------------- */
+static int run_batch_impl(const qo_sys* s, double* psi, int64_t B, const int32_t* act, double f_max,
+                          int n_steps, double dt, double gamma, uint64_t seed, int64_t env_offset,
+                          uint64_t step0, const double* noise, int32_t* fail_step, double* q_out,
+                          double* xm_out, int n_threads) {
+    const int N = s->N;
+    qo_tab* tabs[21];
+    for (int a = 0; a < 21; a++) {
+        double force = (double)(a - 10) * (f_max / 10.);   /* convert_to_force IHO/RL.py:107-111 */
+        tabs[a] = qo_make_tab(s, dt, force, NULL);
+        if (!tabs[a]) { for (int b = 0; b < a; b++) qo_free_tab(tabs[b]); return -1; }
+    }
+    int bad = 0;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t e = 0; e < B; e++) {
+        int a = act ? act[e] : 10;
+        if (a < 0 || a > 20) { bad = 1; continue; }
+        double force = (double)(a - 10) * (f_max / 10.);
+        double* ps = psi + (size_t)e * 2 * N;
+        int32_t fs = 0;
+        for (int k = 0; k < n_steps; k++) {
+            double r[2];
+            if (noise) { r[0] = noise[((size_t)k * B + e) * 2]; r[1] = noise[((size_t)k * B + e) * 2 + 1]; }
+            else qo_normals(seed, (uint64_t)(env_offset + e), step0 + (uint64_t)k, r);
+            double q, xm;
+            int f = 0;
+            qo_step(s, tabs[a], ps, dt, force, gamma, r, &q, &xm, &f);
+            if (f && !fs) fs = k + 1;
+            if (q_out) q_out[(size_t)k * B + e] = q;
+            if (xm_out) xm_out[(size_t)k * B + e] = xm;
+        }
+        if (fail_step) fail_step[e] = fs;
+    }
+    for (int a = 0; a < 21; a++) qo_free_tab(tabs[a]);
+    return bad ? -2 : 0;
+}
+
+int qo_run_batch(const qo_sys* s, double* psi, int64_t B, const int32_t* act, double f_max,
+                 int n_steps, double dt, double gamma, uint64_t seed, int64_t env_offset,
+                 uint64_t step0, int32_t* fail_step, double* q_out, double* xm_out, int n_threads) {
+    return run_batch_impl(s, psi, B, act, f_max, n_steps, dt, gamma, seed, env_offset, step0, NULL,
+                          fail_step, q_out, xm_out, n_threads);
+}
+int qo_run_batch_noise(const qo_sys* s, double* psi, int64_t B, const int32_t* act, double f_max,
+                       int n_steps, double dt, double gamma, const double* noise,
+                       int32_t* fail_step, double* q_out, double* xm_out, int n_threads) {
+    return run_batch_impl(s, psi, B, act, f_max, n_steps, dt, gamma, 0, 0, 0, noise, fail_step,
+                          q_out, xm_out, n_threads);
+}

@@ -1,0 +1,120 @@
+"""ctypes binding of libqcart.so (include/qcart.h).
+
+The library is the only compute path: if it is missing or no HIP device is present, every call
+raises. There is deliberately no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqcart.so")
+
+QC_HO, QC_IHO, QC_QO, QC_IQO = 0, 1, 2, 3
+QC_A_REFERENCE, QC_A_EXACT = 0, 1
+QC_RESET_GROUND, QC_RESET_RANDOM, QC_RESET_GAUSSIAN = 0, 1, 2
+
+STATUS = {
+    0: "QC_OK", -1: "QC_EINVAL", -2: "QC_ENOMEM", -3: "QC_EHIP", -4: "QC_EPIVOT", -5: "QC_ESINGULAR",
+    -6: "QC_ENOTBUILT",
+}
+
+# every symbol include/qcart.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "qc_create", "qc_destroy", "qc_last_error", "qc_abi_version", "qc_get_params", "qc_dim", "qc_n_obs",
+    "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
+    "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
+    "qc_boundary_fail", "qc_reset", "qc_scan_levels",
+)
+
+
+class QcParams(ctypes.Structure):
+    _fields_ = [
+        ("family", ctypes.c_int32),
+        ("n_max", ctypes.c_int32),
+        ("omega", ctypes.c_double),
+        ("x_max", ctypes.c_double),
+        ("grid_size", ctypes.c_double),
+        ("lambda_", ctypes.c_double),
+        ("mass", ctypes.c_double),
+        ("moment_order", ctypes.c_int32),
+        ("a_mode", ctypes.c_int32),
+        ("gamma", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("f_max", ctypes.c_double),
+        ("n_actions", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("batch", ctypes.c_int64),
+        ("env_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("xth", ctypes.c_double),
+    ]
+
+
+class QCartError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def _preload_torch_hip():
+    # Reuse torch's HIP runtime (same SONAME libamdhip64.so.7) so that torch tensors and libqcart
+    # share one runtime, one context and one stream namespace.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()); this package has no CPU fallback")
+    _preload_torch_hip()
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P, vp = ctypes.POINTER, ctypes.c_void_p
+    i32, i64, u64, d = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+    L.qc_create.argtypes = [P(QcParams), ctypes.c_int, P(vp)]
+    L.qc_destroy.argtypes = [vp]
+    L.qc_destroy.restype = None
+    L.qc_last_error.argtypes = [vp]
+    L.qc_last_error.restype = ctypes.c_char_p
+    L.qc_abi_version.argtypes = []
+    L.qc_get_params.argtypes = [vp, P(QcParams)]
+    L.qc_dim.argtypes = [vp]
+    L.qc_n_obs.argtypes = [vp]
+    L.qc_set_stream.argtypes = [vp, vp]
+    L.qc_sync.argtypes = [vp]
+    L.qc_set_seed.argtypes = [vp, u64]
+    L.qc_set_step_counter.argtypes = [vp, u64]
+    L.qc_get_step_counter.argtypes = [vp]
+    L.qc_get_step_counter.restype = u64
+    L.qc_set_dynamics.argtypes = [vp, d, d]
+    L.qc_add_force.argtypes = [vp, d]
+    L.qc_step.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp]
+    L.qc_moments.argtypes = [vp, vp, vp]
+    L.qc_x_expectation.argtypes = [vp, vp, vp]
+    L.qc_outside_prob.argtypes = [vp, vp, d, vp]
+    L.qc_boundary_fail.argtypes = [vp, vp, vp]
+    L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
+    L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
+    for name in EXPORTS:
+        fn = getattr(L, name)
+        if fn.restype is ctypes.c_int:   # default
+            fn.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, handle=None) -> int:
+    if rc < 0:
+        msg = lib().qc_last_error(handle)
+        raise QCartError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,191 @@
+"""Batched device stepper: a thin Python owner of one libqcart handle.
+
+PyTorch is only plumbing here (device memory for psi / actions / observations and the HIP
+stream); every physics operation runs in the HIP kernels behind include/qcart.h.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from .config import Physics
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Stepper:
+    """B environments of one physical system on one device (one handle, one HIP stream)."""
+
+    def __init__(self, physics: Physics, batch: int, device: int | str | torch.device = 0, seed: int = 42,
+                 env_offset: int = 0, xth: float | None = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("libqcart needs a HIP device (no CPU fallback)")
+        self.physics = physics
+        self.batch = int(batch)
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.env_offset = int(env_offset)
+        p = L.QcParams()
+        p.family = physics.family
+        p.n_max = physics.n_max
+        p.omega = physics.omega
+        p.x_max = physics.x_max
+        p.grid_size = physics.grid_size
+        p.lambda_ = physics.lambda_
+        p.mass = physics.mass
+        p.moment_order = physics.moment_order
+        p.a_mode = physics.a_mode
+        p.gamma = physics.gamma
+        p.dt = physics.dt
+        p.f_max = physics.f_max
+        p.n_actions = physics.n_actions
+        p.batch = self.batch
+        p.env_offset = self.env_offset
+        p.seed = seed
+        p.xth = physics.xth if (xth is None and physics.family == 3) else (xth or 0.0)
+        self._params = p
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            torch.cuda.init()
+            L.check(L.lib().qc_create(ctypes.byref(p), self.device.index, ctypes.byref(h)))
+        self._h = h
+        self.N = L.lib().qc_dim(h)
+        self.n_obs = L.lib().qc_n_obs(h)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().qc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        L.check(L.lib().qc_set_stream(self._h, ctypes.c_void_p(s)), self._h)
+
+    def _check_psi(self, psi: torch.Tensor):
+        if psi.dtype != torch.complex128:
+            raise ValueError("The state array does not match the required datatype: Complex128")
+        if psi.dim() != 2 or psi.shape[1] != self.N or psi.shape[0] != self.batch:
+            raise ValueError(f"The state array does not match the required size ({self.batch}, {self.N})")
+        if psi.device != self.device or not psi.is_contiguous():
+            raise ValueError("state must be a contiguous tensor on " + str(self.device))
+
+    # ------------------------------------------------------------------ state helpers
+    def new_state(self) -> torch.Tensor:
+        return torch.zeros((self.batch, self.N), dtype=torch.complex128, device=self.device)
+
+    def set_seed(self, seed: int):
+        L.check(L.lib().qc_set_seed(self._h, seed), self._h)
+
+    @property
+    def step_counter(self) -> int:
+        return int(L.lib().qc_get_step_counter(self._h))
+
+    @step_counter.setter
+    def step_counter(self, v: int):
+        L.check(L.lib().qc_set_step_counter(self._h, int(v)), self._h)
+
+    def set_dynamics(self, dt: float, gamma: float):
+        L.check(L.lib().qc_set_dynamics(self._h, dt, gamma), self._h)
+
+    def add_force(self, force: float) -> int:
+        return L.check(L.lib().qc_add_force(self._h, float(force)), self._h)
+
+    def scan_levels(self, action: int):
+        f, b = ctypes.c_int32(), ctypes.c_int32()
+        L.check(L.lib().qc_scan_levels(self._h, action, ctypes.byref(f), ctypes.byref(b)), self._h)
+        return f.value, b.value
+
+    # ------------------------------------------------------------------ hot path
+    def step(self, psi: torch.Tensor, actions: Optional[torch.Tensor] = None, n_steps: int = 1,
+             default_action: int | None = None, noise: Optional[torch.Tensor] = None, want_q: bool = False,
+             want_fail: bool = True, want_term: bool = False, want_obs: bool = False) -> dict:
+        """Advance every env n_steps physics steps in place (the reference's simulation.step,
+        fused). Returns a dict of device tensors (q, x_mean, fail_step, term_step, obs)."""
+        self._check_psi(psi)
+        B = self.batch
+        if actions is not None:
+            if actions.dtype != torch.int32 or actions.shape != (B,) or actions.device != self.device:
+                raise ValueError("actions must be an int32 tensor of shape (B,) on the handle's device")
+            actions = actions.contiguous()
+        if default_action is None:
+            default_action = self.physics.n_actions // 2
+        if noise is not None:
+            if noise.dtype != torch.float64 or tuple(noise.shape) != (n_steps, B, 2) or noise.device != self.device:
+                raise ValueError("noise must be float64 (n_steps, B, 2) on the handle's device")
+            noise = noise.contiguous()
+        out = {}
+        dev = self.device
+        q = torch.empty((n_steps, B), dtype=torch.float64, device=dev) if want_q else None
+        xm = torch.empty((n_steps, B), dtype=torch.float64, device=dev) if want_q else None
+        fs = torch.empty((B,), dtype=torch.int32, device=dev) if want_fail else None
+        ts = torch.empty((B,), dtype=torch.int32, device=dev) if want_term else None
+        ob = torch.empty((B, self.n_obs), dtype=torch.float64, device=dev) if want_obs else None
+        self._bind_stream()
+        L.check(L.lib().qc_step(self._h, _ptr(psi), _ptr(actions), int(default_action), int(n_steps), _ptr(noise),
+                                _ptr(q), _ptr(xm), _ptr(fs), _ptr(ts), _ptr(ob)), self._h)
+        if want_q:
+            out["q"], out["x_mean"] = q, xm
+        if want_fail:
+            out["fail_step"] = fs
+        if want_term:
+            out["term_step"] = ts
+        if want_obs:
+            out["obs"] = ob
+        return out
+
+    def moments(self, psi: torch.Tensor) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch, self.n_obs), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_moments(self._h, _ptr(psi), _ptr(out)), self._h)
+        return out
+
+    def x_expectation(self, psi: torch.Tensor) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch,), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_x_expectation(self._h, _ptr(psi), _ptr(out)), self._h)
+        return out
+
+    def outside_prob(self, psi: torch.Tensor, xth: float) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch,), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_outside_prob(self._h, _ptr(psi), float(xth), _ptr(out)), self._h)
+        return out
+
+    def boundary_fail(self, psi: torch.Tensor) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch,), dtype=torch.int32, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_boundary_fail(self._h, _ptr(psi), _ptr(out)), self._h)
+        return out
+
+    def reset(self, psi: torch.Tensor, kind: int, mask: Optional[torch.Tensor] = None, arg0: float = 0.0,
+              arg1: float = 0.0, arg2: float = 1.0, k: Optional[torch.Tensor] = None,
+              mean: Optional[torch.Tensor] = None, std: Optional[torch.Tensor] = None):
+        self._check_psi(psi)
+        if mask is not None:
+            mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        for t in (k, mean, std):
+            if t is not None and (t.dtype != torch.float64 or t.shape != (self.batch,)):
+                raise ValueError("per-env reset parameters must be float64 (B,)")
+        self._bind_stream()
+        L.check(L.lib().qc_reset(self._h, _ptr(psi), kind, _ptr(mask), arg0, arg1, arg2, _ptr(k), _ptr(mean),
+                                 _ptr(std)), self._h)
+
+    def sync(self):
+        L.check(L.lib().qc_sync(self._h), self._h)

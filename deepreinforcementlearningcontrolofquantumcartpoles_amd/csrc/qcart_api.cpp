@@ -1,0 +1,453 @@
+// qcart_api.cpp — implementation of the C ABI declared in include/qcart.h.
+//
+// A handle is bound to one device and one HIP stream and owns the operator rows and the per-slot
+// factor tables (21 discrete forces + registered custom forces). All compute runs in the HIP
+// kernels of qcart_kernels.hip; there is no CPU fallback: a missing device or kernel is an error.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/qcart.h"
+#include "qcart_kargs.hpp"
+#include "qcart_tables.hpp"
+
+using namespace qcart;
+
+namespace {
+constexpr int kMaxSlots = 64;
+std::mutex g_err_mu;
+std::string g_create_err;
+
+void set_create_err(const std::string& s) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_create_err = s;
+}
+}  // namespace
+
+struct qc_handle {
+    qc_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int R = 0;
+    bool mirror = false;
+    OpHost op;
+    std::vector<ActHost> acts;
+    uint64_t step = 0;
+    std::string err;
+    // device buffers
+    double *d_xu = nullptr, *d_xg = nullptr, *d_hu = nullptr;
+    double *d_lc = nullptr, *d_uc = nullptr, *d_dinv = nullptr, *d_m2 = nullptr;
+    double *d_tf = nullptr, *d_tb = nullptr, *d_force = nullptr;
+    int32_t *d_kf = nullptr, *d_kb = nullptr;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int fail(qc_handle* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+int hip_check(qc_handle* h, hipError_t e, const char* what) {
+    if (e == hipSuccess) return QC_OK;
+    return fail(h, QC_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// the rows-per-lane instantiations compiled in qcart_kernels.hip
+int pick_R(int family, int N) {
+    static const int r_fock_ho[] = {1, 2, 4, 8};
+    static const int r_fock_iho[] = {1, 2, 3, 4, 8, 16};
+    static const int r_grid[] = {1, 2, 3, 5, 9, 17};
+    const int need = (N + kWave - 1) / kWave;
+    const int* list = family == QC_HO ? r_fock_ho : (family == QC_IHO ? r_fock_iho : r_grid);
+    const int n = family == QC_HO ? 4 : 6;
+    for (int i = 0; i < n; i++)
+        if (list[i] >= need) return list[i];
+    return -1;
+}
+
+void free_dev(qc_handle* h) {
+    double** dp[] = {&h->d_xu, &h->d_xg, &h->d_hu, &h->d_lc, &h->d_uc, &h->d_dinv, &h->d_m2, &h->d_tf, &h->d_tb,
+                     &h->d_force};
+    for (auto p : dp)
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
+    if (h->d_kb) { (void)hipFree(h->d_kb); h->d_kb = nullptr; }
+}
+
+template <typename T>
+int upload(qc_handle* h, T** dst, const T* src, size_t n) {
+    if (!*dst) {
+        hipError_t e = hipMalloc((void**)dst, n * sizeof(T));
+        if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    return hip_check(h, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+// (re)build every slot's tables on the host and upload them (slot capacity kMaxSlots)
+int upload_tables(qc_handle* h) {
+    const int Np = h->op.Npad, kl = h->op.kl;
+    const size_t n_lc = (size_t)kMaxSlots * kl * Np * 2;
+    const size_t n_di = (size_t)kMaxSlots * Np * 2;
+    const size_t n_m2 = (size_t)kMaxSlots * kMirrorBands * Np;
+    const size_t blk = (size_t)kMaxLevels * kWave * kl * kl * 2;
+    std::vector<double> lc(n_lc, 0.0), uc(n_lc, 0.0), di(n_di, 0.0), m2(n_m2, 0.0);
+    std::vector<double> tf((size_t)kMaxSlots * blk, 0.0), tb((size_t)kMaxSlots * blk, 0.0), force(kMaxSlots, 0.0);
+    std::vector<int32_t> kf(kMaxSlots, 0), kb(kMaxSlots, 0);
+    for (size_t s = 0; s < h->acts.size(); s++) {
+        const ActHost& a = h->acts[s];
+        std::memcpy(&lc[s * kl * Np * 2], a.lc.data(), sizeof(double) * kl * Np * 2);
+        std::memcpy(&uc[s * kl * Np * 2], a.uc.data(), sizeof(double) * kl * Np * 2);
+        std::memcpy(&di[s * Np * 2], a.dinv.data(), sizeof(double) * Np * 2);
+        std::memcpy(&m2[s * kMirrorBands * Np], a.m2.data(), sizeof(double) * kMirrorBands * Np);
+        std::memcpy(&tf[s * blk], a.tf.data(), sizeof(double) * blk);
+        std::memcpy(&tb[s * blk], a.tb.data(), sizeof(double) * blk);
+        force[s] = a.force;
+        kf[s] = a.kf;
+        kb[s] = a.kb;
+    }
+    int rc;
+    if ((rc = upload(h, &h->d_lc, lc.data(), lc.size()))) return rc;
+    if ((rc = upload(h, &h->d_uc, uc.data(), uc.size()))) return rc;
+    if ((rc = upload(h, &h->d_dinv, di.data(), di.size()))) return rc;
+    if ((rc = upload(h, &h->d_m2, m2.data(), m2.size()))) return rc;
+    if ((rc = upload(h, &h->d_tf, tf.data(), tf.size()))) return rc;
+    if ((rc = upload(h, &h->d_tb, tb.data(), tb.size()))) return rc;
+    if ((rc = upload(h, &h->d_force, force.data(), force.size()))) return rc;
+    if ((rc = upload(h, &h->d_kf, kf.data(), kf.size()))) return rc;
+    if ((rc = upload(h, &h->d_kb, kb.data(), kb.size()))) return rc;
+    return QC_OK;
+}
+
+int build_all_actions(qc_handle* h) {
+    std::vector<double> forces;
+    for (auto& a : h->acts) forces.push_back(a.force);
+    if (forces.empty())
+        for (int a = 0; a < h->p.n_actions; a++)
+            forces.push_back((double)(a - h->p.n_actions / 2) * (h->p.f_max / (double)(h->p.n_actions / 2)));
+    h->acts.assign(forces.size(), ActHost());
+    for (size_t i = 0; i < forces.size(); i++) {
+        int rc = build_action(h->op, h->p.dt, forces[i], h->mirror, h->acts[i], h->err);
+        if (rc) return rc;
+    }
+    return QC_OK;
+}
+
+KArgs base_args(const qc_handle* h) {
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    const qc_params& p = h->p;
+    const OpHost& op = h->op;
+    a.B = p.batch;
+    a.env_offset = p.env_offset;
+    a.seed = p.seed;
+    a.step0 = h->step;
+    a.N = op.N;
+    a.Npad = op.Npad;
+    a.n_slots = (int32_t)h->acts.size();
+    a.mirror = h->mirror ? 1 : 0;
+    a.bnd_len = op.fock ? 5 : 6;
+    a.win_lo = a.win_hi = 0;
+    if (!op.fock && p.xth > 0) {
+        const int c = op.N / 2, w = (int)std::nearbyint(p.xth / op.h);   // IQO/main_parallel.py:78-81
+        a.win_lo = c - w;
+        a.win_hi = c + w;
+    }
+    a.moment_order = op.fock ? 0 : p.moment_order;
+    a.n_obs = qc_n_obs(h);
+    a.dt = p.dt;
+    a.sqrt_dt = std::sqrt(p.dt);
+    a.gamma = p.gamma;
+    a.g4 = p.gamma / 4.;
+    a.beta = std::sqrt(p.gamma / 2.);
+    a.inv_sqrt2g = 1.0 / std::sqrt(2. * p.gamma);
+    a.w = op.w;
+    a.inv_sqrt_w = 1.0 / std::sqrt(op.w);
+    a.c = op.c;
+    a.h = op.fock ? 1.0 : op.h;
+    const double dt = p.dt;
+    a.a2 = dt * dt * dt / 12.;
+    a.a3 = dt * dt * dt * dt / 24.;
+    a.a4 = dt * dt * dt * dt * dt / 80.;
+    a.a5 = dt * dt * dt * dt * dt * dt / 360.;
+    // check_boundary_error thresholds: IHO 2e-3 (IHO:423), HO 1e-3 (HO:404), grid 5e-3 (QO:561)
+    a.fail_thr = p.family == QC_HO ? 1e-3 : (p.family == QC_IHO ? 2e-3 : 5e-3);
+    for (int d = 0; d < 5; d++) a.hoff[d] = op.hoff[d];
+    a.xu = h->d_xu;
+    a.xg = h->d_xg;
+    a.hu = h->d_hu;
+    a.lc = h->d_lc;
+    a.uc = h->d_uc;
+    a.dinv = h->d_dinv;
+    a.m2 = h->d_m2;
+    a.tf = h->d_tf;
+    a.tb = h->d_tb;
+    a.kf = h->d_kf;
+    a.kb = h->d_kb;
+    a.force = h->d_force;
+    return a;
+}
+
+int validate_params(const qc_params* p, std::string& err) {
+    if (!p) { err = "null params"; return QC_EINVAL; }
+    if (p->family < QC_HO || p->family > QC_IQO) { err = "family must be 0..3"; return QC_EINVAL; }
+    if (!(p->dt > 0) || !std::isfinite(p->dt)) { err = "dt must be > 0"; return QC_EINVAL; }
+    if (!(p->gamma >= 0) || !std::isfinite(p->gamma)) { err = "gamma must be >= 0"; return QC_EINVAL; }
+    if (p->batch < 0) { err = "batch must be >= 0"; return QC_EINVAL; }
+    if (p->n_actions < 1 || p->n_actions > kMaxSlots || (p->n_actions % 2) == 0) {
+        err = "n_actions must be odd and <= 64";
+        return QC_EINVAL;
+    }
+    if (p->family >= QC_QO && (p->moment_order < 1 || p->moment_order > 6)) {
+        err = "moment_order must be in 1..6";
+        return QC_EINVAL;
+    }
+    if (p->a_mode != QC_A_REFERENCE && p->a_mode != QC_A_EXACT) { err = "bad a_mode"; return QC_EINVAL; }
+    return QC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qc_abi_version(void) { return QC_ABI_VERSION; }
+
+const char* qc_last_error(const qc_handle* h) {
+    if (h) return h->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    return g_create_err.c_str();
+}
+
+int qc_create(const qc_params* p, int device, qc_handle** out) {
+    if (!out) { set_create_err("null out"); return QC_EINVAL; }
+    *out = nullptr;
+    std::string err;
+    int rc = validate_params(p, err);
+    if (rc) { set_create_err(err); return rc; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_create_err("no HIP device available (libqcart has no CPU fallback)");
+        return QC_EHIP;
+    }
+    if (device < 0 || device >= ndev) { set_create_err("device index out of range"); return QC_EINVAL; }
+    qc_handle* h = new qc_handle();
+    h->p = *p;
+    h->device = device;
+    h->mirror = (p->family == QC_IHO && p->a_mode == QC_A_REFERENCE);
+    // probe N first to pick the rows-per-lane instantiation
+    OpHost probe;
+    rc = build_ops(p->family, p->n_max, p->omega, p->x_max, p->grid_size, p->lambda_, p->mass, 1 << 12, probe, err);
+    if (rc) { set_create_err(err); delete h; return rc; }
+    h->R = pick_R(p->family, probe.N);
+    if (h->R < 0 || !have_kernel(p->family, h->R)) {
+        set_create_err("no kernel instantiated for N = " + std::to_string(probe.N));
+        delete h;
+        return QC_ENOTBUILT;
+    }
+    rc = build_ops(p->family, p->n_max, p->omega, p->x_max, p->grid_size, p->lambda_, p->mass, h->R, h->op, err);
+    if (rc) { set_create_err(err); delete h; return rc; }
+    rc = build_all_actions(h);
+    if (rc) { set_create_err(h->err); delete h; return rc; }
+    DeviceGuard g(device);
+    const int Np = h->op.Npad;
+    if ((rc = upload(h, &h->d_xu, h->op.xu.data(), Np)) || (rc = upload(h, &h->d_xg, h->op.xg.data(), Np)) ||
+        (rc = upload(h, &h->d_hu, h->op.hu.data(), Np)) || (rc = upload_tables(h))) {
+        set_create_err(h->err);
+        free_dev(h);
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return QC_OK;
+}
+
+void qc_destroy(qc_handle* h) {
+    if (!h) return;
+    {
+        DeviceGuard g(h->device);
+        (void)hipDeviceSynchronize();
+        free_dev(h);
+    }
+    delete h;
+}
+
+int qc_get_params(const qc_handle* h, qc_params* out) {
+    if (!h || !out) return QC_EINVAL;
+    *out = h->p;
+    return QC_OK;
+}
+
+int qc_dim(const qc_handle* h) { return h ? h->op.N : QC_EINVAL; }
+
+int qc_n_obs(const qc_handle* h) {
+    if (!h) return QC_EINVAL;
+    if (h->op.fock) return 5;
+    const int m = h->p.moment_order;
+    return (2 + m + 1) * m / 2;   // QO/simulation_quart.cpp:381
+}
+
+int qc_set_stream(qc_handle* h, void* stream) {
+    if (!h) return QC_EINVAL;
+    h->stream = (hipStream_t)stream;
+    return QC_OK;
+}
+
+int qc_sync(qc_handle* h) {
+    if (!h) return QC_EINVAL;
+    DeviceGuard g(h->device);
+    return hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+}
+
+int qc_set_seed(qc_handle* h, uint64_t seed) {
+    if (!h) return QC_EINVAL;
+    h->p.seed = seed;
+    h->step = 0;
+    return QC_OK;
+}
+int qc_set_step_counter(qc_handle* h, uint64_t step) {
+    if (!h) return QC_EINVAL;
+    h->step = step;
+    return QC_OK;
+}
+uint64_t qc_get_step_counter(const qc_handle* h) { return h ? h->step : 0; }
+
+int qc_set_dynamics(qc_handle* h, double dt, double gamma) {
+    if (!h) return QC_EINVAL;
+    if (!(dt > 0) || !(gamma >= 0)) return fail(h, QC_EINVAL, "dt must be > 0 and gamma >= 0");
+    const bool change_t = dt != h->p.dt;
+    h->p.gamma = gamma;
+    if (!change_t) return QC_OK;
+    const double old = h->p.dt;
+    h->p.dt = dt;
+    int rc = build_all_actions(h);
+    if (rc) {
+        h->p.dt = old;
+        build_all_actions(h);
+        return rc;
+    }
+    DeviceGuard g(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    return upload_tables(h);
+}
+
+int qc_add_force(qc_handle* h, double force) {
+    if (!h) return QC_EINVAL;
+    for (size_t s = 0; s < h->acts.size(); s++)
+        if (h->acts[s].force == force) return (int)s;
+    if ((int)h->acts.size() >= kMaxSlots) return fail(h, QC_ENOMEM, "no free force slot");
+    ActHost a;
+    int rc = build_action(h->op, h->p.dt, force, h->mirror, a, h->err);
+    if (rc) return rc;
+    h->acts.push_back(a);
+    DeviceGuard g(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    rc = upload_tables(h);
+    if (rc) { h->acts.pop_back(); return rc; }
+    return (int)h->acts.size() - 1;
+}
+
+int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_action, int32_t n_steps,
+            const double* noise, double* q_out, double* xmean_out, int32_t* fail_step, int32_t* term_step,
+            double* obs_out) {
+    if (!h) return QC_EINVAL;
+    if (!psi && h->p.batch > 0) return fail(h, QC_EINVAL, "psi is null");
+    if (n_steps < 0) return fail(h, QC_EINVAL, "n_steps must be >= 0");
+    if (!actions && (default_action < 0 || default_action >= (int)h->acts.size()))
+        return fail(h, QC_EINVAL, "default_action out of range");
+    if (term_step && !(h->p.xth > 0 && !h->op.fock))
+        return fail(h, QC_EINVAL, "term_step needs a grid family and params.xth > 0");
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    a.actions = actions;
+    a.default_action = default_action;
+    a.n_steps = n_steps;
+    a.noise = noise;
+    a.q_out = q_out;
+    a.xm_out = xmean_out;
+    a.fail_step = fail_step;
+    a.term_step = term_step;
+    a.obs_out = obs_out;
+    DeviceGuard g(h->device);
+    int rc = launch_step(h->p.family, h->R, a, h->stream);
+    if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
+    h->step += (uint64_t)n_steps;
+    return QC_OK;
+}
+
+int qc_moments(qc_handle* h, const void* psi, double* out) {
+    if (!h || (!psi && h->p.batch > 0) || (!out && h->p.batch > 0)) return QC_EINVAL;
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    a.obs_out = out;
+    DeviceGuard g(h->device);
+    int rc = launch_obs(h->p.family, h->R, a, h->stream);
+    return rc ? fail(h, rc, "obs kernel launch failed") : QC_OK;
+}
+
+int qc_x_expectation(qc_handle* h, const void* psi, double* out) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 0, a, 0.0, out, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
+int qc_outside_prob(qc_handle* h, const void* psi, double xth, double* out) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    if (h->op.fock) return fail(h, QC_EINVAL, "outside probability is defined on grid families");
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 1, a, xth, out, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
+int qc_boundary_fail(qc_handle* h, const void* psi, int32_t* out) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 2, a, 0.0, out, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
+int qc_reset(qc_handle* h, void* psi, int32_t kind, const uint8_t* mask, double arg0, double arg1, double arg2,
+             const double* k_arr, const double* mean_arr, const double* std_arr) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    if (kind < QC_RESET_GROUND || kind > QC_RESET_GAUSSIAN) return fail(h, QC_EINVAL, "bad reset kind");
+    if (kind == QC_RESET_GAUSSIAN && h->op.fock) return fail(h, QC_EINVAL, "Gaussian packet needs a grid family");
+    if (kind != QC_RESET_GAUSSIAN && !h->op.fock) return fail(h, QC_EINVAL, "Fock reset needs a Fock family");
+    if (kind == QC_RESET_RANDOM && !(arg0 >= 1)) return fail(h, QC_EINVAL, "levels must be >= 1");
+    if (kind == QC_RESET_GAUSSIAN && !std_arr && !(arg2 > 0)) return fail(h, QC_EINVAL, "std must be > 0");
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_reset(h->p.family, h->R, a, kind, mask, arg0, arg1, arg2, k_arr, mean_arr, std_arr, h->stream);
+    return rc ? fail(h, rc, "reset kernel launch failed") : QC_OK;
+}
+
+int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {
+    if (!h || action < 0 || action >= (int)h->acts.size()) return QC_EINVAL;
+    if (fwd) *fwd = h->acts[action].kf;
+    if (bwd) *bwd = h->acts[action].kb;
+    return QC_OK;
+}
+
+}  // extern "C"

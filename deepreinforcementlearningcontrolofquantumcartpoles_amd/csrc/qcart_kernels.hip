@@ -1,0 +1,933 @@
+// qcart_kernels.hip — CDNA4 (gfx950) kernels for the quantum-cartpole env.step() hot path.
+//
+// One 64-lane wavefront owns one environment; lane l holds rows [l*R, l*R + R) of psi (and of
+// every intermediate vector) in VGPRs for the whole call, so n_steps physics steps run with psi
+// resident in registers and HBM is touched once per call (load + store of psi).
+//
+// Per physics step the wave executes the reference scheme (IHO/simulation_i.cpp:
+// 432-489, HO/simulation.cpp:413-470, QO/simulation_quart.cpp:569-624):
+//   * X / H / H_F stencils: banded, real coefficients, lane-boundary halos by cross-lane shuffles
+//   * 3 wave reductions per step: (Y+, Y-) means, (Phi+, Phi-) means, (norm, next <x>, Fail
+//     boundary sums, IQO window) fused into one
+//   * term7 = A D1 by Horner in H_F (5 stencil passes) + the IHO MKL-HERMITIAN mirror correction
+//   * the banded Crank-Nicolson solve (zgbtrs) as a two-pass lane-local recurrence joined by a
+//     Kogge-Stone scan over lanes with precomputed composite transfer matrices
+//   * counter-based Philox4x32-10 noise: lane j generates the normals of step k0 + j, one
+//     Box-Muller per lane per 64 steps, broadcast with v_readlane.
+// No MFMA: there is no dense contraction (FP64 VALU-bound).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qcart_kargs.hpp"
+
+namespace qcart {
+
+struct cd {
+    double re, im;
+};
+__device__ __forceinline__ cd C(double r, double i) {
+    cd c;
+    c.re = r;
+    c.im = i;
+    return c;
+}
+__device__ __forceinline__ cd cmul(cd a, cd b) { return C(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re); }
+__device__ __forceinline__ cd cmac(cd acc, cd a, cd b) {   // acc + a*b
+    return C(acc.re + a.re * b.re - a.im * b.im, acc.im + a.re * b.im + a.im * b.re);
+}
+__device__ __forceinline__ cd cmsub(cd acc, cd a, cd b) {  // acc - a*b
+    return C(acc.re - (a.re * b.re - a.im * b.im), acc.im - (a.re * b.im + a.im * b.re));
+}
+__device__ __forceinline__ cd ld(const double* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
+    unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int NV>
+__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off, 64);
+    }
+}
+
+// ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
+template <int FAM>
+struct Fam;
+template <>
+struct Fam<0> { static constexpr int KL = 1; };
+template <>
+struct Fam<1> { static constexpr int KL = 2; };
+template <>
+struct Fam<2> { static constexpr int KL = 4; };
+
+// ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t
+template <int R, int H>
+__device__ __forceinline__ void make_ext(const cd (&v)[R], cd (&e)[R + 2 * H], int lane) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) e[H + j] = v[j];
+#pragma unroll
+    for (int t = 0; t < H; ++t) {
+        const int o = H - t;
+        const int dl = (o + R - 1) / R;
+        const int idx = dl * R - o;
+        double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
+        const bool ok = lane >= dl;
+        e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+    }
+#pragma unroll
+    for (int t = 0; t < H; ++t) {
+        const int o = R + t;
+        const int dl = o / R;
+        const int idx = o - dl * R;
+        double re = __shfl_down(v[idx].re, dl, 64), im = __shfl_down(v[idx].im, dl, 64);
+        const bool ok = lane + dl < 64;
+        e[H + R + t] = C(ok ? re : 0.0, ok ? im : 0.0);
+    }
+}
+// lower halo only: e[t] = row base - H + t, t < H
+template <int R, int H>
+__device__ __forceinline__ void make_lo(const cd (&v)[R], cd (&e)[H], int lane) {
+#pragma unroll
+    for (int t = 0; t < H; ++t) {
+        const int o = H - t;
+        const int dl = (o + R - 1) / R;
+        const int idx = dl * R - o;
+        double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
+        const bool ok = lane >= dl;
+        e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+    }
+}
+
+// ---- per-lane operator coefficients (action independent), loaded once per call
+template <int FAM, int R>
+struct Coef {
+    double xu[R + 1];  // Fock: X[base-1+t][base+t]
+    double hu[R + 2];  // IHO: H[base-2+t][base+t]; HO / grid: H[base+t][base+t]
+    double xg[R];      // grid: x_{base+t}
+    int base, N;
+    double hoff[5];
+};
+
+template <int FAM, int R>
+__device__ __forceinline__ void load_coef(Coef<FAM, R>& cf, const KArgs& a, int base) {
+    cf.base = base;
+    cf.N = a.N;
+    if constexpr (FAM <= 1) {
+#pragma unroll
+        for (int t = 0; t <= R; ++t) {
+            int r = base - 1 + t;
+            cf.xu[t] = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
+        }
+    }
+    if constexpr (FAM == 1) {
+#pragma unroll
+        for (int t = 0; t < R + 2; ++t) {
+            int r = base - 2 + t;
+            cf.hu[t] = (r >= 0 && r < a.Npad) ? a.hu[r] : 0.0;
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < R; ++t) cf.hu[t] = a.hu[base + t];
+    }
+    if constexpr (FAM == 2) {
+#pragma unroll
+        for (int t = 0; t < R; ++t) cf.xg[t] = a.xg[base + t];
+#pragma unroll
+        for (int d = 0; d < 5; ++d) cf.hoff[d] = a.hoff[d];
+    }
+}
+
+// X v   (IHO/simulation_i.cpp:168-196 Fock tridiagonal; QO/simulation_quart.cpp:214-229 grid diag)
+template <int FAM, int R>
+__device__ __forceinline__ void apply_x(const cd (&v)[R], cd (&o)[R], const Coef<FAM, R>& cf, int lane) {
+    if constexpr (FAM <= 1) {
+        cd e[R + 2];
+        make_ext<R, 1>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            o[j] = C(cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re,
+                     cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im);
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) o[j] = C(cf.xg[j] * v[j].re, cf.xg[j] * v[j].im);
+    }
+}
+
+// H v and X v with one halo exchange
+template <int FAM, int R>
+__device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)[R], const Coef<FAM, R>& cf,
+                                         int lane) {
+    if constexpr (FAM == 0) {
+        apply_x<FAM, R>(v, ox, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) oh[j] = C(cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
+    } else if constexpr (FAM == 1) {
+        cd e[R + 4];
+        make_ext<R, 2>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            ox[j] = C(cf.xu[j + 1] * e[j + 3].re + cf.xu[j] * e[j + 1].re,
+                      cf.xu[j + 1] * e[j + 3].im + cf.xu[j] * e[j + 1].im);
+            oh[j] = C(cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re,
+                      cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
+        }
+    } else {
+        cd e[R + 8];
+        make_ext<R, 4>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            ox[j] = C(cf.xg[j] * v[j].re, cf.xg[j] * v[j].im);
+            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+#pragma unroll
+            for (int d = 1; d <= 4; ++d) {
+                re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
+                im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
+            }
+            const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
+            oh[j] = C(in ? re : 0.0, in ? im : 0.0);
+        }
+    }
+}
+
+// u = H_F v = H v - cF X v
+template <int FAM, int R>
+__device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF, const Coef<FAM, R>& cf,
+                                         int lane) {
+    cd hx[R], xx[R];
+    apply_hx<FAM, R>(v, hx, xx, cf, lane);
+#pragma unroll
+    for (int j = 0; j < R; ++j) u[j] = C(hx[j].re - cF * xx[j].re, hx[j].im - cF * xx[j].im);
+}
+
+// ---- counter-based noise (oracle: qo_normals)
+__device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
+        const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+    }
+}
+__device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ctr, uint32_t tag, double& r0,
+                                        double& r1) {
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), env, tag};
+    philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t a = ((((uint64_t)c[0]) << 32) | c[1]) >> 11;
+    const uint64_t b = ((((uint64_t)c[2]) << 32) | c[3]) >> 11;
+    const double u1 = ((double)a + 0.5) * 0x1.0p-53;
+    const double u2 = ((double)b + 0.5) * 0x1.0p-53;
+    const double rad = sqrt(-2.0 * log(u1));
+    double s, co;
+    sincos(2.0 * M_PI * u2, &s, &co);
+    r0 = rad * co;
+    r1 = rad * s;
+}
+
+// ---- banded solve (zgbtrs, IHO/simulation_i.cpp:487, QO/simulation_quart.cpp:622) of the
+// precomputed pivot-free LU, in place on b.
+template <int KL, int R>
+__device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict__ lc, const double* __restrict__ uc,
+                                           const double* __restrict__ dinv, const double* __restrict__ tf,
+                                           const double* __restrict__ tb, int kf, int kb, int lane, int base,
+                                           int Np) {
+    // forward, pass 1 (zero incoming state): lane end state e_l
+    cd s[KL];
+#pragma unroll
+    for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        cd y = b[j];
+#pragma unroll
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, ld(lc, (size_t)k * Np + base + j), s[k]);
+#pragma unroll
+        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+        s[0] = y;
+    }
+    // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
+    for (int lvl = 0; lvl < kf; ++lvl) {
+        const int d = 1 << lvl;
+        cd p[KL];
+#pragma unroll
+        for (int k = 0; k < KL; ++k) p[k] = C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
+        if (lane >= d) {
+            const double* T = tf + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
+#pragma unroll
+            for (int i = 0; i < KL; ++i)
+#pragma unroll
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], ld(T, i * KL + k), p[k]);
+        }
+    }
+    // incoming state from lane - 1, pass 2
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+        double re = __shfl_up(s[k].re, 1, 64), im = __shfl_up(s[k].im, 1, 64);
+        s[k] = (lane >= 1) ? C(re, im) : C(0.0, 0.0);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        cd y = b[j];
+#pragma unroll
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, ld(lc, (size_t)k * Np + base + j), s[k]);
+#pragma unroll
+        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+        s[0] = y;
+        b[j] = y;
+    }
+    // backward, pass 1 (rows high -> low): x_r = dinv_r y_r - sum_k uc_k x_{r+k}
+#pragma unroll
+    for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
+#pragma unroll
+    for (int j = R - 1; j >= 0; --j) {
+        cd x = cmul(ld(dinv, base + j), b[j]);
+#pragma unroll
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ld(uc, (size_t)k * Np + base + j), s[k]);
+#pragma unroll
+        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+        s[0] = x;
+    }
+    for (int lvl = 0; lvl < kb; ++lvl) {
+        const int d = 1 << lvl;
+        cd p[KL];
+#pragma unroll
+        for (int k = 0; k < KL; ++k) p[k] = C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
+        if (lane + d < 64) {
+            const double* T = tb + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
+#pragma unroll
+            for (int i = 0; i < KL; ++i)
+#pragma unroll
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], ld(T, i * KL + k), p[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+        double re = __shfl_down(s[k].re, 1, 64), im = __shfl_down(s[k].im, 1, 64);
+        s[k] = (lane + 1 < 64) ? C(re, im) : C(0.0, 0.0);
+    }
+#pragma unroll
+    for (int j = R - 1; j >= 0; --j) {
+        cd x = cmul(ld(dinv, base + j), b[j]);
+#pragma unroll
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ld(uc, (size_t)k * Np + base + j), s[k]);
+#pragma unroll
+        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+        s[0] = x;
+        b[j] = x;
+    }
+}
+
+// ---- observations ---------------------------------------------------------------------------
+// Fock 'xp' (IHO/main_parallel.py:129-131): [<x>, <p>, <x^2>-<x>^2, <p^2>-<p>^2, <xp+px>/2-<x><p>]
+// with the truncated operators: <x^2> = |X psi|^2, <p^2> = |P psi|^2, <xp+px>/2 = Re<X psi, P psi>.
+template <int FAM, int R>
+__device__ __forceinline__ void fock_obs(const cd (&psi)[R], const Coef<FAM, R>& cf, int lane, double (&o)[5]) {
+    cd e[R + 2];
+    make_ext<R, 1>(psi, e, lane);
+    double s[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const cd xp = C(cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re, cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im);
+        // P psi = i (xu[r-1] psi_{r-1} - xu[r] psi_{r+1})
+        const cd t = C(cf.xu[j] * e[j].re - cf.xu[j + 1] * e[j + 2].re, cf.xu[j] * e[j].im - cf.xu[j + 1] * e[j + 2].im);
+        const cd pp = C(-t.im, t.re);
+        s[0] += psi[j].re * xp.re + psi[j].im * xp.im;
+        s[1] += psi[j].re * pp.re + psi[j].im * pp.im;
+        s[2] += xp.re * xp.re + xp.im * xp.im;
+        s[3] += pp.re * pp.re + pp.im * pp.im;
+        s[4] += xp.re * pp.re + xp.im * pp.im;
+    }
+    wave_sum<5>(s);
+    o[0] = s[0];
+    o[1] = s[1];
+    o[2] = s[2] - s[0] * s[0];
+    o[3] = s[3] - s[1] * s[1];
+    o[4] = s[4] - s[0] * s[1];
+}
+
+// grid p_hat (minus pbar) under the reference's HERMITIAN/UPPER descriptor with its truncated
+// Delta_1 loops (QO/simulation_quart.cpp:59-70, :283-286): upper (r, r+d) exists iff r <= N-1-2d.
+template <int R>
+__device__ __forceinline__ void grid_p(const cd (&v)[R], cd (&o)[R], double pbar, double inv_h, int N, int base,
+                                       int lane) {
+    cd e[R + 8];
+    make_ext<R, 4>(v, e, lane);
+    const double sd[5] = {0.0, 672.0 / 840.0, -168.0 / 840.0, 32.0 / 840.0, -3.0 / 840.0};
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int r = base + j;
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int d = 1; d <= 4; ++d) {
+            const double dl = sd[d] * inv_h;
+            const double up = (r <= N - 1 - 2 * d) ? dl : 0.0;
+            const double dn = (r <= N - 1 - d) ? dl : 0.0;
+            re += up * e[4 + j + d].re - dn * e[4 + j - d].re;
+            im += up * e[4 + j + d].im - dn * e[4 + j - d].im;
+        }
+        // (-i) * (re + i im) - pbar v
+        const bool in = r < N;
+        o[j] = C(in ? im - pbar * v[j].re : 0.0, in ? -re - pbar * v[j].im : 0.0);
+    }
+}
+
+constexpr int kMaxMoment = 6;                 // obs vector up to (2+6+1)*6/2 = 27
+constexpr int kMaxObs = (2 + kMaxMoment + 1) * kMaxMoment / 2;
+
+// compute_statistics (QO/simulation_quart.cpp:326-362)
+template <int R>
+__device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, int lane, int m, double h,
+                                         double (&o)[kMaxObs]) {
+    const double inv_h = 1.0 / h;
+    cd v[R];
+    double s2[2] = {0, 0};
+    grid_p<R>(psi, v, 0.0, inv_h, cf.N, cf.base, lane);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        s2[0] += cf.xg[j] * (psi[j].re * psi[j].re + psi[j].im * psi[j].im);
+        s2[1] += psi[j].re * v[j].re + psi[j].im * v[j].im;
+    }
+    wave_sum<2>(s2);
+    const double xbar = s2[0] * h, pbar = s2[1] * h;
+    double acc[kMaxObs];
+#pragma unroll
+    for (int i = 0; i < kMaxObs; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = psi[j];
+#pragma unroll
+    for (int b = 0; b <= kMaxMoment; ++b) {
+        if (b > m) break;
+        if (b > 0) {
+            cd nv[R];
+            grid_p<R>(v, nv, pbar, inv_h, cf.N, cf.base, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = nv[j];
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double xr = cf.xg[j] - xbar;
+            const double base_re = psi[j].re * v[j].re + psi[j].im * v[j].im;   // Re conj(psi) v
+            double xa = 1.0;
+#pragma unroll
+            for (int aa = 0; aa <= kMaxMoment; ++aa) {
+                const int jj = aa + b;
+                if (jj >= 2 && jj <= kMaxMoment) {
+                    const int idx = 2 + (jj - 2) * (jj + 3) / 2 + b;
+                    acc[idx] += xa * base_re;
+                }
+                xa *= xr;
+            }
+        }
+    }
+    wave_sum<kMaxObs>(acc);
+    o[0] = xbar;
+    o[1] = pbar;
+#pragma unroll
+    for (int i = 2; i < kMaxObs; ++i) o[i] = acc[i] * h;
+}
+
+// ---- the fused multi-step kernel ------------------------------------------------------------
+template <int FAM, int R>
+__global__ __launch_bounds__(256) void k_step(const KArgs a) {
+    constexpr int KL = Fam<FAM>::KL;
+    const int lane = threadIdx.x & 63;
+    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (env >= a.B) return;
+    const int base = lane * R;
+    const int N = a.N, Np = a.Npad;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+
+    int slot = a.actions ? a.actions[env] : a.default_action;
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
+    const double cF = a.c * a.force[slot];
+    const double* lc = a.lc + (size_t)slot * KL * Np * 2;
+    const double* uc = a.uc + (size_t)slot * KL * Np * 2;
+    const double* dinv = a.dinv + (size_t)slot * Np * 2;
+    const double* m2 = a.m2 + (size_t)slot * 10 * Np;
+    const double* tf = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const double* tb = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const int kf = a.kf[slot], kb = a.kb[slot];
+
+    double* gpsi = a.psi + (size_t)env * N * 2;
+    cd psi[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+
+    const bool win_on = a.win_hi > a.win_lo;
+    cd xp[R];
+    apply_x<FAM, R>(psi, xp, cf, lane);
+    double xbar;
+    int term = -1, fail = 0;
+    {
+        double s[2] = {0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            s[0] += psi[j].re * xp[j].re + psi[j].im * xp[j].im;
+            const int r = base + j;
+            if (r >= a.win_lo && r < a.win_hi) s[1] += psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+        }
+        wave_sum<2>(s);
+        xbar = a.w * s[0];                                        // x_expct (IHO:197-203, QO:230-236)
+        if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
+    }
+    const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
+    const uint32_t genv = (uint32_t)(a.env_offset + env);
+    double nz0 = 0.0, nz1 = 0.0;
+
+    for (int k = 0; k < a.n_steps; ++k) {
+        if ((k & 63) == 0) {   // lane j: normals of step k + j
+            if (a.noise) {
+                const int kk = k + lane;
+                if (kk < a.n_steps) {
+                    nz0 = a.noise[((size_t)kk * a.B + env) * 2];
+                    nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
+                }
+            } else {
+                normals(a.seed, genv, a.step0 + (uint64_t)(k + lane), 0u, nz0, nz1);
+            }
+        }
+        const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
+        // go_one_step: IHO/simulation_i.cpp:432-489
+        const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 / 1.7320508075688772);
+        if (lane == 0) {
+            if (a.q_out) a.q_out[(size_t)k * a.B + env] = xbar + dW * a.inv_sqrt2g / dt;
+            if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = xbar;
+        }
+        const double c1 = 0.5 / sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 / sdt * (dW * dW - dt);
+        const double c4 = 0.5 / dt * (dW * dt - dZ), c5 = 0.25 / dt * (dW * dW / 3 - dt) * dW;
+        const double c6 = 0.25 * sdt * dW;
+
+        cd acc[R], Yp[R], Ym[R];
+        {
+            // D1 (IHO:279-298), D2 (IHO:320-333)
+            cd rel[R], D1[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
+            {
+                cd hp[R], xr[R], tmp[R];
+                apply_hx<FAM, R>(psi, hp, tmp, cf, lane);
+                apply_x<FAM, R>(rel, xr, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double hre = hp[j].re - cF * xp[j].re, him = hp[j].im - cF * xp[j].im;
+                    const double qre = xr[j].re - xbar * rel[j].re, qim = xr[j].im - xbar * rel[j].im;
+                    D1[j] = C(him - g4 * qre, -hre - g4 * qim);
+                }
+            }
+            const double kA = (dW - 2.0 * c4) * beta, kY = sdt * beta, k2 = 2.0 * c2;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re, psi[j].im + kA * rel[j].im + k2 * D1[j].im);
+                const double yr = psi[j].re + dt * D1[j].re, yi = psi[j].im + dt * D1[j].im;
+                Yp[j] = C(yr + kY * rel[j].re, yi + kY * rel[j].im);
+                Ym[j] = C(yr - kY * rel[j].re, yi - kY * rel[j].im);
+            }
+            // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)   (IHO:253-264, :551)
+            {
+                cd t[R], u[R];
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(-a.a5 * D1[j].im, a.a5 * D1[j].re);
+                apply_hf<FAM, R>(t, u, cF, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(u[j].re - a.a4 * D1[j].re, u[j].im - a.a4 * D1[j].im);
+                apply_hf<FAM, R>(t, u, cF, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(u[j].re + a.a3 * D1[j].im, u[j].im - a.a3 * D1[j].re);
+                apply_hf<FAM, R>(t, u, cF, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(u[j].re + a.a2 * D1[j].re, u[j].im + a.a2 * D1[j].im);
+                apply_hf<FAM, R>(t, u, cF, cf, lane);
+                apply_hf<FAM, R>(u, t, cF, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) acc[j] = C(acc[j].re + t[j].re, acc[j].im + t[j].im);
+            }
+            if constexpr (FAM == 1) {
+                // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  
+                if (a.mirror) {
+                    cd lo[10];
+                    make_lo<R, 10>(D1, lo, lane);
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        double sre = 0.0, sim = 0.0;
+#pragma unroll
+                        for (int d = 1; d <= 10; ++d) {
+                            const double mv = m2[(size_t)(d - 1) * Np + base + j];
+                            const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
+                                                       : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
+                            sre += mv * dv.re;
+                            sim += mv * dv.im;
+                        }
+                        acc[j] = C(acc[j].re + sim, acc[j].im - sre);
+                    }
+                }
+            }
+        }
+        // Y+- (D1ImRe IHO:301-318 + D2 precomputed), unnormalised means
+        double yp, ym;
+        {
+            cd xYp[R], xYm[R];
+            apply_x<FAM, R>(Yp, xYp, cf, lane);
+            apply_x<FAM, R>(Ym, xYm, cf, lane);
+            double s[2] = {0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                s[0] += Yp[j].re * xYp[j].re + Yp[j].im * xYp[j].im;
+                s[1] += Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im;
+            }
+            wave_sum<2>(s);
+            yp = a.w * s[0];
+            ym = a.w * s[1];
+            const double kIm = c1 - c6;
+            // + branch
+            {
+                cd hY[R], xx[R];
+                apply_hx<FAM, R>(Yp, hY, xx, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double hre = hY[j].re - cF * xYp[j].re, him = hY[j].im - cF * xYp[j].im;
+                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) * (-i H_F Y+)
+                    xYp[j] = C(xYp[j].re - yp * Yp[j].re, xYp[j].im - yp * Yp[j].im);   // rel+
+                }
+                cd xr[R];
+                apply_x<FAM, R>(xYp, xr, cf, lane);
+                const double kRe = -(c1 + c2) * g4, kD = (c3 + c4 - c5) * beta, kP = sdt * beta;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double qre = xr[j].re - yp * xYp[j].re, qim = xr[j].im - yp * xYp[j].im;
+                    acc[j] = C(acc[j].re + kRe * qre + kD * xYp[j].re, acc[j].im + kRe * qim + kD * xYp[j].im);
+                    const cd pp = C(Yp[j].re + kP * xYp[j].re, Yp[j].im + kP * xYp[j].im);    // Phi+
+                    const cd pm = C(Yp[j].re - kP * xYp[j].re, Yp[j].im - kP * xYp[j].im);    // Phi-
+                    Yp[j] = pp;
+                    xYp[j] = pm;
+                }
+            }
+            // - branch
+            {
+                cd hY[R], xx[R];
+                apply_hx<FAM, R>(Ym, hY, xx, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double hre = hY[j].re - cF * xYm[j].re, him = hY[j].im - cF * xYm[j].im;
+                    acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);   // -(c1-c6) * (-i H_F Y-)
+                    xYm[j] = C(xYm[j].re - ym * Ym[j].re, xYm[j].im - ym * Ym[j].im);   // rel-
+                }
+                cd xr[R];
+                apply_x<FAM, R>(xYm, xr, cf, lane);
+                const double kRe = -(c2 - c1) * g4, kD = (c4 - c3 + c5) * beta;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double qre = xr[j].re - ym * xYm[j].re, qim = xr[j].im - ym * xYm[j].im;
+                    acc[j] = C(acc[j].re + kRe * qre + kD * xYm[j].re, acc[j].im + kRe * qim + kD * xYm[j].im);
+                }
+            }
+            // Phi+- : D2 with fresh unnormalised means (IHO:321-332, :480)
+            {
+                cd xPp[R], xPm[R];
+                apply_x<FAM, R>(Yp, xPp, cf, lane);
+                apply_x<FAM, R>(xYp, xPm, cf, lane);
+                double t2[2] = {0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    t2[0] += Yp[j].re * xPp[j].re + Yp[j].im * xPp[j].im;
+                    t2[1] += xYp[j].re * xPm[j].re + xYp[j].im * xPm[j].im;
+                }
+                wave_sum<2>(t2);
+                const double pp = a.w * t2[0], pm = a.w * t2[1], k5 = c5 * beta;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    acc[j] = C(acc[j].re + k5 * ((xPp[j].re - pp * Yp[j].re) - (xPm[j].re - pm * xYp[j].re)),
+                               acc[j].im + k5 * ((xPp[j].im - pp * Yp[j].im) - (xPm[j].im - pm * xYp[j].im)));
+                }
+            }
+        }
+        // implicit Crank-Nicolson solve (IHO:487)
+        band_solve<KL, R>(acc, lc, uc, dinv, tf, tb, kf, kb, lane, base, Np);
+        // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
+        {
+            cd xn[R];
+            apply_x<FAM, R>(acc, xn, cf, lane);
+            double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const double p2 = acc[j].re * acc[j].re + acc[j].im * acc[j].im;
+                s[0] += p2;
+                s[1] += acc[j].re * xn[j].re + acc[j].im * xn[j].im;
+                const int r = base + j;
+                if (r >= N - a.bnd_len && r < N) s[2] += p2;
+                if (r < a.bnd_len) s[3] += p2;
+                if (r >= a.win_lo && r < a.win_hi) s[4] += p2;
+            }
+            wave_sum<5>(s);
+            double scale = 1.0 / sqrt(s[0]);
+            if constexpr (FAM == 2) scale = scale * a.inv_sqrt_w;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                psi[j] = C(acc[j].re * scale, acc[j].im * scale);
+                xp[j] = C(xn[j].re * scale, xn[j].im * scale);
+            }
+            xbar = a.w * (s[1] * scale) * scale;
+            bool f = sqrt(s[2]) * scale > a.fail_thr;
+            if constexpr (FAM == 2) f = f || (sqrt(s[3]) * scale > a.fail_thr);
+            if (f && fail == 0) fail = k + 1;
+            if (win_on && term < 0 && 1.0 - a.h * (s[4] * scale) * scale > 0.5) term = k + 1;
+        }
+    }
+    // write back
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (base + j < N) {
+            gpsi[2 * (base + j)] = psi[j].re;
+            gpsi[2 * (base + j) + 1] = psi[j].im;
+        }
+    if (lane == 0) {
+        if (a.fail_step) a.fail_step[env] = fail;
+        if (a.term_step) a.term_step[env] = term;
+    }
+    if (a.obs_out) {
+        if constexpr (FAM <= 1) {
+            double o[5];
+            fock_obs<FAM, R>(psi, cf, lane, o);
+            if (lane < 5) {
+                double v = o[0];
+#pragma unroll
+                for (int i = 1; i < 5; ++i) v = (lane == i) ? o[i] : v;
+                a.obs_out[(size_t)env * 5 + lane] = v;
+            }
+        } else {
+            double o[kMaxObs];
+            grid_obs<R>(psi, cf, lane, a.moment_order, a.h, o);
+            if (lane < a.n_obs) {
+                double v = o[0];
+#pragma unroll
+                for (int i = 1; i < kMaxObs; ++i) v = (lane == i) ? o[i] : v;
+                a.obs_out[(size_t)env * a.n_obs + lane] = v;
+            }
+        }
+    }
+}
+
+// ---- standalone observation / aux / reset kernels --------------------------------------------
+template <int FAM, int R>
+__global__ __launch_bounds__(256) void k_obs(const KArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (env >= a.B) return;
+    const int base = lane * R;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+    const double* gpsi = a.psi + (size_t)env * a.N * 2;
+    cd psi[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < a.N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+    if constexpr (FAM <= 1) {
+        double o[5];
+        fock_obs<FAM, R>(psi, cf, lane, o);
+        if (lane < 5) {
+            double v = o[0];
+#pragma unroll
+            for (int i = 1; i < 5; ++i) v = (lane == i) ? o[i] : v;
+            a.obs_out[(size_t)env * 5 + lane] = v;
+        }
+    } else {
+        double o[kMaxObs];
+        grid_obs<R>(psi, cf, lane, a.moment_order, a.h, o);
+        if (lane < a.n_obs) {
+            double v = o[0];
+#pragma unroll
+            for (int i = 1; i < kMaxObs; ++i) v = (lane == i) ? o[i] : v;
+            a.obs_out[(size_t)env * a.n_obs + lane] = v;
+        }
+    }
+}
+
+// what: 0 = x_expectation (double), 1 = outside probability (double), 2 = boundary Fail (int32)
+template <int FAM, int R>
+__global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth, void* out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (env >= a.B) return;
+    const int base = lane * R, N = a.N;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+    const double* gpsi = a.psi + (size_t)env * N * 2;
+    cd psi[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+    double s[3] = {0.0, 0.0, 0.0};
+    if (what == 0) {
+        cd xp[R];
+        apply_x<FAM, R>(psi, xp, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[0] += psi[j].re * xp[j].re + psi[j].im * xp[j].im;
+    } else if (what == 1) {
+        const int c = N / 2, w = (int)rint(xth / a.h);   // Python round(): ties to even
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int r = base + j;
+            if (r >= c - w && r < c + w) s[0] += psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int r = base + j;
+            const double p2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+            if (r >= N - a.bnd_len && r < N) s[1] += p2;
+            if (r < a.bnd_len) s[2] += p2;
+        }
+    }
+    wave_sum<3>(s);
+    if (lane == 0) {
+        if (what == 0) ((double*)out)[env] = s[0] * a.w;
+        else if (what == 1) ((double*)out)[env] = 1.0 - s[0] * a.h;
+        else {
+            bool f = sqrt(s[1]) > a.fail_thr;
+            if (FAM == 2) f = f || sqrt(s[2]) > a.fail_thr;
+            ((int32_t*)out)[env] = f ? 1 : 0;
+        }
+    }
+}
+
+template <int FAM, int R>
+__global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const uint8_t* mask, double a0, double a1,
+                                                double a2, const double* k_arr, const double* m_arr,
+                                                const double* s_arr) {
+    const int lane = threadIdx.x & 63;
+    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (env >= a.B) return;
+    if (mask && !mask[env]) return;
+    const int base = lane * R, N = a.N;
+    double* gpsi = a.psi + (size_t)env * N * 2;
+    cd v[R];
+    if (kind == 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = C(base + j == 0 ? 1.0 : 0.0, 0.0);
+    } else if (kind == 1) {
+        const int levels = (int)a0;
+        double s[1] = {0.0};
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int r = base + j;
+            if (r < levels && r < N) {
+                double r0, r1;
+                normals(a.seed, (uint32_t)(a.env_offset + env), (uint64_t)r, 1u, r0, r1);
+                v[j] = C(r0, r1);
+                s[0] += r0 * r0 + r1 * r1;
+            } else {
+                v[j] = C(0.0, 0.0);
+            }
+        }
+        wave_sum<1>(s);
+        const double sc = 1.0 / sqrt(s[0]);
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = C(v[j].re * sc, v[j].im * sc);
+    } else {
+        const double k = k_arr ? k_arr[env] : a0, mu = m_arr ? m_arr[env] : a1, sg = s_arr ? s_arr[env] : a2;
+        const double nrm = sqrt(sqrt(2.0 * M_PI) * sg);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int r = base + j;
+            const double x = (r < N) ? a.xg[r] : 0.0;
+            const double ph = 2.0 * M_PI * (x - mu) * k;
+            const double g = exp(-(x - mu) * (x - mu) / (4.0 * sg * sg)) / nrm;
+            double sn, cs;
+            sincos(ph, &sn, &cs);
+            v[j] = C(cs * g, sn * g);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (base + j < N) {
+            gpsi[2 * (base + j)] = v[j].re;
+            gpsi[2 * (base + j) + 1] = v[j].im;
+        }
+}
+
+// ---- dispatch ---------------------------------------------------------------------------------
+#define QC_FOR_EACH_R0(X) X(0, 1) X(0, 2) X(0, 4) X(0, 8)
+#define QC_FOR_EACH_R1(X) X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(1, 8) X(1, 16)
+#define QC_FOR_EACH_R2(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(2, 9) X(2, 17)
+#define QC_FOR_ALL(X) QC_FOR_EACH_R0(X) QC_FOR_EACH_R1(X) QC_FOR_EACH_R2(X)
+
+static int fam_of(int family) { return family <= 1 ? family : 2; }
+
+static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
+
+bool have_kernel(int family, int R) {
+    const int F = fam_of(family);
+#define QC_HAVE(FF, RR) \
+    if (F == FF && R == RR) return true;
+    QC_FOR_ALL(QC_HAVE)
+#undef QC_HAVE
+    return false;
+}
+
+int launch_step(int family, int R, const KArgs& a, void* stream) {
+    const int F = fam_of(family);
+    if (a.B <= 0) return 0;
+#define QC_LAUNCH(FF, RR)                                                                              \
+    if (F == FF && R == RR) {                                                                          \
+        hipLaunchKernelGGL((k_step<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a); \
+        return hipGetLastError() == hipSuccess ? 0 : -3;                                               \
+    }
+    QC_FOR_ALL(QC_LAUNCH)
+#undef QC_LAUNCH
+    return -6;
+}
+
+int launch_obs(int family, int R, const KArgs& a, void* stream) {
+    const int F = fam_of(family);
+    if (a.B <= 0) return 0;
+#define QC_LAUNCH(FF, RR)                                                                             \
+    if (F == FF && R == RR) {                                                                         \
+        hipLaunchKernelGGL((k_obs<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a); \
+        return hipGetLastError() == hipSuccess ? 0 : -3;                                              \
+    }
+    QC_FOR_ALL(QC_LAUNCH)
+#undef QC_LAUNCH
+    return -6;
+}
+
+int launch_aux(int family, int R, int what, const KArgs& a, double xth, void* out, void* stream) {
+    const int F = fam_of(family);
+    if (a.B <= 0) return 0;
+#define QC_LAUNCH(FF, RR)                                                                                   \
+    if (F == FF && R == RR) {                                                                               \
+        hipLaunchKernelGGL((k_aux<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a, what, \
+                           xth, out);                                                                       \
+        return hipGetLastError() == hipSuccess ? 0 : -3;                                                    \
+    }
+    QC_FOR_ALL(QC_LAUNCH)
+#undef QC_LAUNCH
+    return -6;
+}
+
+int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mask, double a0, double a1,
+                 double a2, const double* k_arr, const double* m_arr, const double* s_arr, void* stream) {
+    const int F = fam_of(family);
+    if (a.B <= 0) return 0;
+#define QC_LAUNCH(FF, RR)                                                                                     \
+    if (F == FF && R == RR) {                                                                                 \
+        hipLaunchKernelGGL((k_reset<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a, kind, \
+                           mask, a0, a1, a2, k_arr, m_arr, s_arr);                                            \
+        return hipGetLastError() == hipSuccess ? 0 : -3;                                                      \
+    }
+    QC_FOR_ALL(QC_LAUNCH)
+#undef QC_LAUNCH
+    return -6;
+}
+
+}  // namespace qcart

@@ -1,0 +1,163 @@
+/*
+ * qcart.h — C ABI of libqcart.so, the MI355X-native quantum-cartpole env.step() hot path.
+ *
+ * Drop-in boundary for the reference CPython extension `simulation` (one module per physical
+ * system, compiled by each directory setupC.py with -D macros). Each entry point below names the reference
+ * function it replaces (file:line; aliases as in SURVEY.md: HO/ IHO/ QO/ IQO/ =
+ * "implementation codes/{harmonic, inverted harmonic, quartic, inverted quartic} oscillator/").
+ *
+ * Conventions
+ *  - Plain C types only. Every psi / output pointer is a DEVICE pointer (hipMalloc'd or a torch
+ *    tensor's data_ptr()) on the handle's device unless stated otherwise.
+ *  - psi layout: [B][N] complex fp64, interleaved (re, im) — the numpy complex128 layout the
+ *    reference takes (IHO/simulation_i.cpp:374-376), batched env-major.
+ *  - All launches are asynchronous on the handle's stream (qc_set_stream; default: the null
+ *    stream); qc_sync() fences.
+ *  - Return value: 0 on success, < 0 on error (never aborts); qc_last_error() explains.
+ *    Reference counterpart: Python exceptions (TypeError/ValueError/RuntimeError,
+ *    IHO/simulation_i.cpp:340-372, QO/simulation_quart.cpp:288-323, :517).
+ */
+#ifndef QCART_H
+#define QCART_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QC_ABI_VERSION 1
+
+/* physical systems (one reference directory each) */
+enum qc_family {
+    QC_HO = 0,   /* harmonic cooling, Fock basis, H = omega (n + 1/2)       HO/simulation.cpp        */
+    QC_IHO = 1,  /* inverted harmonic cartpole, H = -omega/2 (a+^2 + a^2)   IHO/simulation_i.cpp     */
+    QC_QO = 2,   /* quartic cooling, 8th-order FD grid, lambda > 0          QO/simulation_quart.cpp  */
+    QC_IQO = 3   /* inverted quartic cartpole, lambda < 0                   IQO/simulation_quart.cpp */
+};
+
+/* semantics of the dt^3..dt^6 correction product term7 = A . D1 */
+enum qc_a_mode {
+    QC_A_REFERENCE = 0, /* the reference's MKL descriptor: IHO HERMITIAN/UPPER mirror, others exact */
+    QC_A_EXACT = 1      /* the intended complex-symmetric A                                          */
+};
+
+enum qc_status {
+    QC_OK = 0,
+    QC_EINVAL = -1,     /* bad argument / shape (reference: ValueError)                 */
+    QC_ENOMEM = -2,
+    QC_EHIP = -3,       /* HIP runtime error                                            */
+    QC_EPIVOT = -4,     /* band LU would need row interchanges       */
+    QC_ESINGULAR = -5,
+    QC_ENOTBUILT = -6   /* no kernel instantiated for this (family, N)                  */
+};
+
+/* Runtime replacement of setupC.py's compile-time macros (HO/setupC.py:49, QO/setupC.py:55)
+ * plus the per-call step() arguments dt / gamma that are fixed for a batch. */
+typedef struct qc_params {
+    int32_t family;        /* enum qc_family                                                     */
+    int32_t n_max;         /* Fock: N = n_max + 1  (N_MAX macro)                                 */
+    double omega;          /* Fock: OMEGA macro (the drivers pass pi)                           */
+    double x_max;          /* grid: X_MAX;  x_n = 2*int(x_max/grid_size + 0.5) + 1              */
+    double grid_size;      /* grid: GRID_SIZE (h)                                                */
+    double lambda_;        /* grid: LAMBDA (already multiplied by pi, IQO/main_parallel.py:29)  */
+    double mass;           /* grid: MASS (already divided by pi)                                 */
+    int32_t moment_order;  /* grid: MOMENT macro (default 5 -> 20 observables)                  */
+    int32_t a_mode;        /* enum qc_a_mode                                                     */
+    double gamma;          /* measurement strength (step() argument; the drivers pass args.gamma*pi) */
+    double dt;             /* time step (step() argument; 1/time_steps)                         */
+    double f_max;          /* action -> force map F = (a - 10) * f_max / 10 (IHO/RL.py:107-111)  */
+    int32_t n_actions;     /* 21 (2*10 + 1, IHO/RL.py:81,94)                                     */
+    int32_t reserved0;
+    int64_t batch;         /* B envs held by this handle (this rank's shard)                   */
+    int64_t env_offset;    /* global id of env 0 (multi-GPU sharding keeps noise invariant)    */
+    uint64_t seed;         /* Philox key (replaces set_seed's MT19937 stream, IHO:574-579)     */
+    double xth;            /* IQO per-step outside-probability window half-width (0 = off)      */
+} qc_params;
+
+typedef struct qc_handle qc_handle;
+
+/* Module init: Set_World ctor + PyInit (IHO/simulation_i.cpp:26-151, :643-653;
+ * QO/simulation_quart.cpp:28-209). Builds the operator bands and the per-action factor tables
+ * (reset_ab, IHO:227-277 / QO:394-432) for all n_actions forces on `device`. */
+int qc_create(const qc_params* p, int device, qc_handle** out);
+void qc_destroy(qc_handle* h);
+const char* qc_last_error(const qc_handle* h);   /* h may be NULL: last qc_create failure */
+int qc_abi_version(void);
+
+/* check_settings() (IHO/simulation_i.cpp:581-583, QO/simulation_quart.cpp:652-654) */
+int qc_get_params(const qc_handle* h, qc_params* out);
+int qc_dim(const qc_handle* h);                  /* N = n_max+1 or x_n */
+int qc_n_obs(const qc_handle* h);                /* 5 (Fock 'xp') or (2+m+1)*m/2 (grid) */
+
+/* Stream binding (a hipStream_t passed as void*; NULL = default stream). */
+int qc_set_stream(qc_handle* h, void* stream);
+int qc_sync(qc_handle* h);
+
+/* set_seed(int) (IHO/simulation_i.cpp:574-579): re-keys the counter-based noise and resets the
+ * step counter. */
+int qc_set_seed(qc_handle* h, uint64_t seed);
+int qc_set_step_counter(qc_handle* h, uint64_t step);
+uint64_t qc_get_step_counter(const qc_handle* h);
+
+/* Change dt / gamma (step()'s per-call arguments; reset_ab on dt change, IHO:377-383). */
+int qc_set_dynamics(qc_handle* h, double dt, double gamma);
+
+/* Register an arbitrary force (step(state, dt, force, gamma) with a force off the 21-level grid,
+ * e.g. the reference's analytic controllers before rounding). Returns a slot >= n_actions usable
+ * as an action index, or < 0. Slots are cached by force value. */
+int qc_add_force(qc_handle* h, double force);
+
+/*
+ * step() / simulate_10_steps() (IHO/simulation_i.cpp:358-421, HO/simulation.cpp:339-402,
+ * QO/simulation_quart.cpp:493-558), batched and fused over n_steps physics steps:
+ *   psi       [B][N] complex128, advanced in place (the reference mutates `state` in place).
+ *   actions   [B] int32 action index per env (0..n_actions-1 or a qc_add_force slot);
+ *             NULL -> every env uses `default_action`.
+ *   noise     [n_steps][B][2] fp64 N(0,1) draws to inject (parity tests), or NULL for the
+ *             in-kernel Philox4x32-10 stream keyed by (seed, env_offset + e, step counter).
+ *   q_out, xmean_out  [n_steps][B] per-step (q, x_mean) outputs of step(), or NULL.
+ *   fail_step [B]: 1-based index of the first step after which Fail (check_boundary_error) held,
+ *             0 if none; NULL to skip.
+ *   term_step [B]: IQO outside-probability criterion (IQO/main_parallel.py:78-81,199-200) on the
+ *             states before each step and after the last: first k in [0, n_steps] with
+ *             P_out > 0.5, -1 if none; requires params.xth > 0; NULL to skip.
+ *   obs_out   [B][n_obs] fp64 observation of the final state (same as qc_moments), or NULL.
+ * The step counter advances by n_steps.
+ */
+int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_action, int32_t n_steps,
+            const double* noise, double* q_out, double* xmean_out, int32_t* fail_step,
+            int32_t* term_step, double* obs_out);
+
+/* get_moments(state, out) (QO/simulation_quart.cpp:363-388) for grids; the Fock 'xp' vector
+ * get_data_xp (IHO/main_parallel.py:129-131) for HO/IHO. out [B][n_obs] fp64. */
+int qc_moments(qc_handle* h, const void* psi, double* out);
+
+/* x_expectation(state) (IHO/simulation_i.cpp:204-215, QO/simulation_quart.cpp:244-258): out [B] */
+int qc_x_expectation(qc_handle* h, const void* psi, double* out);
+
+/* calculate_outside_probability(state, xth) (IQO/main_parallel.py:78-81): out [B] */
+int qc_outside_prob(qc_handle* h, const void* psi, double xth, double* out);
+
+/* check_boundary_error (IHO/simulation_i.cpp:422-426, QO/simulation_quart.cpp:559-565): out [B] */
+int qc_boundary_fail(qc_handle* h, const void* psi, int32_t* out);
+
+/* Episode reset of psi for envs with mask[e] != 0 (mask NULL = all; device uint8 [B]):
+ *   QC_RESET_GROUND   Fock |0> (IHO/main_parallel.py:231-232, HO/main_parallel.py:226-227)
+ *   QC_RESET_RANDOM   Fock: normalised complex Gaussian amplitudes on levels < arg0 (synthetic
+ *                     benchmark input), Philox stream tag 1 keyed by global env id
+ *   QC_RESET_GAUSSIAN grid: Gaussian_packet(wavelength=1/k, mean, std) (IQO/main_parallel.py:75-76,
+ *                     182-183) with per-env k/mean/std (device fp64 [B] arrays, may be NULL ->
+ *                     arg0/arg1/arg2 scalars) */
+enum qc_reset_kind { QC_RESET_GROUND = 0, QC_RESET_RANDOM = 1, QC_RESET_GAUSSIAN = 2 };
+int qc_reset(qc_handle* h, void* psi, int32_t kind, const uint8_t* mask, double arg0, double arg1,
+             double arg2, const double* k_arr, const double* mean_arr, const double* std_arr);
+
+/* Host-side introspection of the factor tables (tests): number of Kogge-Stone levels kept for
+ * action a (forward, backward), and the truncation bound used. */
+int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,223 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU restatement (oracle/) on identical
+inputs and identical Wiener noise.
+
+Tolerance (BASELINE.json north_star): ||psi_GPU - psi_ref||_2 < 1e-9 after 1000 steps, fp64.
+The oracle is the checker only (parity vs the reference binary itself is unpinned, see
+oracle/qcart_oracle.h).
+"""
+from math import pi, sqrt
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper  # noqa: E402
+
+TOL_1000 = 1e-9
+
+
+def oracle_sys(oracle_mod, ph):
+    return oracle_mod.OracleSystem(ph.family, n_max=ph.n_max, omega=ph.omega, x_max=ph.x_max,
+                                   grid_size=ph.grid_size, lambda_=ph.lambda_, mass=ph.mass,
+                                   moment_order=ph.moment_order, a_mode=ph.a_mode)
+
+
+def init_states(osys, ph, B, seed=1234):
+    if ph.fock:
+        return np.stack([osys.fock_random_state(seed, e, 16) for e in range(B)])
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(B):
+        psi = osys.gaussian_packet(rng.uniform(-0.3, 0.3), rng.uniform(-1, 1), rng.uniform(0.7, 1.3))
+        psi /= np.linalg.norm(psi) * sqrt(ph.grid_size)
+        out.append(psi)
+    return np.stack(out)
+
+
+def wnorm(ph, v):
+    return np.linalg.norm(v, axis=-1) * (sqrt(ph.grid_size) if not ph.fock else 1.0)
+
+
+CASES = {
+    "iho64": cfg.DEFAULTS[cfg.IHO].with_(n_max=63),
+    "iho181": cfg.DEFAULTS[cfg.IHO],
+    "iho512": cfg.DEFAULTS[cfg.IHO].with_(n_max=511),
+    "iho512_exact": cfg.DEFAULTS[cfg.IHO].with_(n_max=511, a_mode=1),
+    "ho256": cfg.DEFAULTS[cfg.HO].with_(n_max=255),
+    "ho71": cfg.DEFAULTS[cfg.HO],
+    "qo171": cfg.DEFAULTS[cfg.QO],
+    "iqo513": cfg.DEFAULTS[cfg.IQO].with_(x_max=12.8),
+}
+
+
+@pytest.mark.parametrize("name,steps,B", [
+    ("iho64", 1000, 8), ("iho181", 1000, 8), ("iho512", 1000, 6), ("iho512_exact", 300, 4),
+    ("ho256", 1000, 6), ("ho71", 1000, 8), ("qo171", 1000, 6), ("iqo513", 400, 4),
+])
+def test_psi_parity_injected_noise(oracle_mod, name, steps, B):
+    ph = CASES[name]
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = init_states(osys, ph, B)
+    rng = np.random.default_rng(7)
+    acts = rng.integers(0, 21, size=B).astype(np.int32)
+    noise = rng.standard_normal((steps, B, 2))
+    ref = psi0.copy()
+    fail_ref, q_ref, xm_ref = osys.run_batch(ref, acts, ph.f_max, steps, ph.dt, ph.gamma, noise=noise,
+                                              want_q=True, n_threads=8)
+    st = Stepper(ph, B, 0)
+    psi = torch.from_numpy(psi0).cuda()
+    out = st.step(psi, torch.from_numpy(acts).cuda(), steps, noise=torch.from_numpy(noise).cuda(), want_q=True)
+    got = psi.cpu().numpy()
+    err = wnorm(ph, got - ref)
+    assert err.max() < TOL_1000, err
+    np.testing.assert_allclose(out["x_mean"].cpu().numpy(), xm_ref, atol=1e-9)
+    np.testing.assert_allclose(out["q"].cpu().numpy(), q_ref, atol=1e-7)
+    assert np.array_equal(out["fail_step"].cpu().numpy(), fail_ref)
+
+
+def test_psi_parity_inkernel_philox(oracle_mod):
+    """In-kernel Philox4x32-10 noise keyed by (seed, global env id, step) reproduces the oracle's."""
+    ph = CASES["iho181"]
+    B, steps, seed, off = 5, 200, 99, 1000
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = init_states(osys, ph, B)
+    acts = np.arange(B, dtype=np.int32) * 4
+    ref = psi0.copy()
+    osys.run_batch(ref, acts, ph.f_max, steps, ph.dt, ph.gamma, seed=seed, env_offset=off, step0=0, n_threads=4)
+    st = Stepper(ph, B, 0, seed=seed, env_offset=off)
+    psi = torch.from_numpy(psi0).cuda()
+    st.step(psi, torch.from_numpy(acts).cuda(), 120)
+    st.step(psi, torch.from_numpy(acts).cuda(), 80)   # counter continues across calls
+    assert st.step_counter == 200
+    assert wnorm(ph, psi.cpu().numpy() - ref).max() < 1e-10
+
+
+def test_split_calls_bitwise_equal():
+    ph = CASES["iho512"]
+    B = 8
+    st1 = Stepper(ph, B, 0, seed=5)
+    st2 = Stepper(ph, B, 0, seed=5)
+    a = st1.new_state()
+    st1.reset(a, 1, arg0=16)
+    b = a.clone()
+    acts = torch.randint(0, 21, (B,), dtype=torch.int32, device="cuda")
+    st1.step(a, acts, 80)
+    st2.step(b, acts, 30)
+    st2.step(b, acts, 50)
+    assert torch.equal(a, b)
+
+
+def test_shard_invariance_bitwise():
+    """1 handle x 8 envs == 2 handles x 4 envs with env_offset (multi-GPU sharding contract)."""
+    ph = CASES["iho181"]
+    full = Stepper(ph, 8, 0, seed=3)
+    s0 = Stepper(ph, 4, 0, seed=3, env_offset=0)
+    s1 = Stepper(ph, 4, 0, seed=3, env_offset=4)
+    a = full.new_state()
+    full.reset(a, 1, arg0=16)
+    acts = torch.randint(0, 21, (8,), dtype=torch.int32, device="cuda")
+    b0, b1 = a[:4].clone(), a[4:].clone()
+    full.step(a, acts, 100)
+    s0.step(b0, acts[:4].contiguous(), 100)
+    s1.step(b1, acts[4:].contiguous(), 100)
+    assert torch.equal(a, torch.cat([b0, b1]))
+
+
+@pytest.mark.parametrize("name", ["iho181", "iho512", "ho71", "qo171", "iqo513"])
+def test_moments_parity(oracle_mod, name):
+    ph = CASES[name]
+    B = 4
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = init_states(osys, ph, B, seed=11)
+    # evolve a little so the states are generic
+    osys.run_batch(psi0, np.full(B, 3, np.int32), ph.f_max, 40, ph.dt, ph.gamma, seed=1, n_threads=4)
+    st = Stepper(ph, B, 0)
+    psi = torch.from_numpy(psi0).cuda()
+    got = st.moments(psi).cpu().numpy()
+    ref = np.stack([osys.moments(p) for p in psi0])
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-11)
+    xe = st.x_expectation(psi).cpu().numpy()
+    np.testing.assert_allclose(xe, [osys.x_expectation(p) for p in psi0], atol=1e-12)
+    bf = st.boundary_fail(psi).cpu().numpy()
+    assert list(bf) == [osys.boundary_fail(p) for p in psi0]
+    # fused observation at the end of a step call equals the standalone kernel
+    out = st.step(psi, None, 0, want_obs=True)
+    np.testing.assert_allclose(out["obs"].cpu().numpy(), got, rtol=0, atol=0)
+
+
+def test_outside_probability_and_term_step(oracle_mod):
+    ph = CASES["iqo513"]
+    B = 3
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = np.stack([osys.gaussian_packet(0.0, mu, 1.0) for mu in (0.0, 3.5, 4.8)])
+    st = Stepper(ph, B, 0)
+    psi = torch.from_numpy(psi0.copy()).cuda()
+    got = st.outside_prob(psi, ph.xth).cpu().numpy()
+    np.testing.assert_allclose(got, [osys.outside_prob(p, ph.xth) for p in psi0], atol=1e-13)
+    # per-step termination index against the oracle
+    steps = 160
+    noise = np.random.default_rng(3).standard_normal((steps, B, 2))
+    acts = np.array([20, 20, 20], np.int32)
+    ref = psi0.copy()
+    term_ref = np.full(B, -1)
+    for e in range(B):
+        if osys.outside_prob(ref[e], ph.xth) > 0.5:
+            term_ref[e] = 0
+    for k in range(steps):
+        osys.run_batch(ref, acts, ph.f_max, 1, ph.dt, ph.gamma, noise=noise[k:k + 1])
+        for e in range(B):
+            if term_ref[e] < 0 and osys.outside_prob(ref[e], ph.xth) > 0.5:
+                term_ref[e] = k + 1
+    out = st.step(psi, torch.from_numpy(acts).cuda(), steps, noise=torch.from_numpy(noise).cuda(), want_term=True)
+    assert list(out["term_step"].cpu().numpy()) == list(term_ref)
+
+
+def test_reset_kernels_match_oracle(oracle_mod):
+    ph = CASES["iho181"]
+    st = Stepper(ph, 6, 0, seed=1234, env_offset=10)
+    osys = oracle_sys(oracle_mod, ph)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=16)
+    ref = np.stack([osys.fock_random_state(1234, 10 + e, 16) for e in range(6)])
+    np.testing.assert_allclose(psi.cpu().numpy(), ref, atol=1e-15)
+    mask = torch.tensor([1, 0, 1, 0, 0, 1], dtype=torch.uint8, device="cuda")
+    st.reset(psi, 0, mask=mask)
+    got = psi.cpu().numpy()
+    assert got[0, 0] == 1 and np.count_nonzero(got[0]) == 1 and np.allclose(got[1], ref[1])
+    g = CASES["iqo513"]
+    sg = Stepper(g, 2, 0)
+    og = oracle_sys(oracle_mod, g)
+    pg = sg.new_state()
+    sg.reset(pg, 2, arg0=0.0, arg1=0.0, arg2=1.0)
+    np.testing.assert_allclose(pg.cpu().numpy()[0], og.gaussian_packet(0.0, 0.0, 1.0), atol=1e-15)
+
+
+def test_scan_truncation_levels_reported():
+    st = Stepper(CASES["iho512"], 1, 0)
+    kf, kb = st.scan_levels(20)
+    assert 1 <= kf <= 6 and 1 <= kb <= 6
+
+
+def test_custom_force_slot_matches_oracle(oracle_mod):
+    ph = CASES["iho181"]
+    osys = oracle_sys(oracle_mod, ph)
+    st = Stepper(ph, 2, 0)
+    slot = st.add_force(1.2345)
+    assert slot >= 21
+    psi0 = init_states(osys, ph, 2)
+    noise = np.random.default_rng(0).standard_normal((100, 2, 2))
+    ref = psi0.copy()
+    for e in range(2):
+        t = ref[e].copy()
+        for k in range(100):
+            osys.step(t, ph.dt, 1.2345, ph.gamma, noise[k, e])
+        ref[e] = t
+    psi = torch.from_numpy(psi0).cuda()
+    st.step(psi, None, 100, default_action=slot, noise=torch.from_numpy(noise).cuda())
+    assert wnorm(ph, psi.cpu().numpy() - ref).max() < 1e-11

@@ -4,8 +4,8 @@ PKG := deepreinforcementlearningcontrolofquantumcartpoles_amd
 CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
-SRCS := $(CSRC)/qcart_kernels.hip $(CSRC)/qcart_api.cpp $(CSRC)/qcart_tables.cpp
-HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp
+OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_dispatch.o qcart_api.o qcart_tables.o)
+HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
 all: $(LIB) oracle
 
@@ -16,14 +16,14 @@ $(CSRC)/build/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/build/qcart_kernels.o $(CSRC)/build/qcart_api.o $(CSRC)/build/qcart_tables.o
+$(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle
 
 resource-usage:
-	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/qcart_kernels.hip -o /tmp/qcart_ru.o -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|LDS" 
+	python3 tools/kernel_resources.py $(CSRC)/build/qcart_k_*.o
 
 clean:
 	rm -rf $(CSRC)/build $(LIB)

@@ -25,7 +25,7 @@ EXPORTS = (
     "qc_create", "qc_destroy", "qc_last_error", "qc_abi_version", "qc_get_params", "qc_dim", "qc_n_obs",
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
-    "qc_boundary_fail", "qc_reset", "qc_scan_levels",
+    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_scan_levels",
 )
 
 
@@ -98,11 +98,13 @@ def lib() -> ctypes.CDLL:
     L.qc_get_step_counter.restype = u64
     L.qc_set_dynamics.argtypes = [vp, d, d]
     L.qc_add_force.argtypes = [vp, d]
-    L.qc_step.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp]
+    L.qc_step.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.qc_moments.argtypes = [vp, vp, vp]
     L.qc_x_expectation.argtypes = [vp, vp, vp]
     L.qc_outside_prob.argtypes = [vp, vp, d, vp]
     L.qc_boundary_fail.argtypes = [vp, vp, vp]
+    L.qc_energy.argtypes = [vp, vp, vp]
+    L.qc_phonon_number.argtypes = [vp, vp, vp]
     L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
     for name in EXPORTS:

@@ -110,7 +110,8 @@ class Stepper:
 
     # ------------------------------------------------------------------ hot path
     def step(self, psi: torch.Tensor, actions: Optional[torch.Tensor] = None, n_steps: int = 1,
-             default_action: int | None = None, noise: Optional[torch.Tensor] = None, want_q: bool = False,
+             default_action: int | None = None, noise: Optional[torch.Tensor] = None,
+             env_steps: Optional[torch.Tensor] = None, want_q: bool = False,
              want_fail: bool = True, want_term: bool = False, want_obs: bool = False) -> dict:
         """Advance every env n_steps physics steps in place (the reference's simulation.step,
         fused). Returns a dict of device tensors (q, x_mean, fail_step, term_step, obs)."""
@@ -122,6 +123,10 @@ class Stepper:
             actions = actions.contiguous()
         if default_action is None:
             default_action = self.physics.n_actions // 2
+        if env_steps is not None:
+            if env_steps.dtype != torch.int32 or env_steps.shape != (B,) or env_steps.device != self.device:
+                raise ValueError("env_steps must be an int32 tensor of shape (B,) on the handle's device")
+            env_steps = env_steps.contiguous()
         if noise is not None:
             if noise.dtype != torch.float64 or tuple(noise.shape) != (n_steps, B, 2) or noise.device != self.device:
                 raise ValueError("noise must be float64 (n_steps, B, 2) on the handle's device")
@@ -134,7 +139,8 @@ class Stepper:
         ts = torch.empty((B,), dtype=torch.int32, device=dev) if want_term else None
         ob = torch.empty((B, self.n_obs), dtype=torch.float64, device=dev) if want_obs else None
         self._bind_stream()
-        L.check(L.lib().qc_step(self._h, _ptr(psi), _ptr(actions), int(default_action), int(n_steps), _ptr(noise),
+        L.check(L.lib().qc_step(self._h, _ptr(psi), _ptr(actions), int(default_action), int(n_steps),
+                                _ptr(env_steps), _ptr(noise),
                                 _ptr(q), _ptr(xm), _ptr(fs), _ptr(ts), _ptr(ob)), self._h)
         if want_q:
             out["q"], out["x_mean"] = q, xm
@@ -172,6 +178,20 @@ class Stepper:
         out = torch.empty((self.batch,), dtype=torch.int32, device=self.device)
         self._bind_stream()
         L.check(L.lib().qc_boundary_fail(self._h, _ptr(psi), _ptr(out)), self._h)
+        return out
+
+    def energy(self, psi: torch.Tensor) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch,), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_energy(self._h, _ptr(psi), _ptr(out)), self._h)
+        return out
+
+    def phonon_number(self, psi: torch.Tensor) -> torch.Tensor:
+        self._check_psi(psi)
+        out = torch.empty((self.batch,), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_phonon_number(self._h, _ptr(psi), _ptr(out)), self._h)
         return out
 
     def reset(self, psi: torch.Tensor, kind: int, mask: Optional[torch.Tensor] = None, arg0: float = 0.0,

@@ -363,7 +363,7 @@ int qc_add_force(qc_handle* h, double force) {
 }
 
 int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_action, int32_t n_steps,
-            const double* noise, double* q_out, double* xmean_out, int32_t* fail_step, int32_t* term_step,
+            const int32_t* env_steps, const double* noise, double* q_out, double* xmean_out, int32_t* fail_step, int32_t* term_step,
             double* obs_out) {
     if (!h) return QC_EINVAL;
     if (!psi && h->p.batch > 0) return fail(h, QC_EINVAL, "psi is null");
@@ -375,6 +375,7 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     KArgs a = base_args(h);
     a.psi = (double*)psi;
     a.actions = actions;
+    a.env_steps = env_steps;
     a.default_action = default_action;
     a.n_steps = n_steps;
     a.noise = noise;
@@ -425,6 +426,25 @@ int qc_boundary_fail(qc_handle* h, const void* psi, int32_t* out) {
     a.psi = (double*)psi;
     DeviceGuard g(h->device);
     int rc = launch_aux(h->p.family, h->R, 2, a, 0.0, out, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
+int qc_energy(qc_handle* h, const void* psi, double* out) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 3, a, 0.0, out, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
+int qc_phonon_number(qc_handle* h, const void* psi, double* out) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    if (!h->op.fock) return fail(h, QC_EINVAL, "phonon number is defined on Fock families");
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 4, a, 0.0, out, h->stream);
     return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
 }
 

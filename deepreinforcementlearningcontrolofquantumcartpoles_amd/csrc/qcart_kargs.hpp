@@ -8,6 +8,7 @@ struct KArgs {
     // state and I/O (device pointers)
     double* psi;               // [B][N] complex interleaved
     const int32_t* actions;    // [B] or null
+    const int32_t* env_steps;  // [B] per-env step budget (min with n_steps) or null
     const double* noise;       // [n_steps][B][2] or null
     double* q_out;             // [n_steps][B] or null
     double* xm_out;            // [n_steps][B] or null

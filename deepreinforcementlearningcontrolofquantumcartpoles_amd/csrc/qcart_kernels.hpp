@@ -1,4 +1,5 @@
-// qcart_kernels.hip — CDNA4 (gfx950) kernels for the quantum-cartpole env.step() hot path.
+#pragma once
+// qcart_kernels.hpp — CDNA4 (gfx950) kernels for the quantum-cartpole env.step() hot path.
 //
 // One 64-lane wavefront owns one environment; lane l holds rows [l*R, l*R + R) of psi (and of
 // every intermediate vector) in VGPRs for the whole call, so n_steps physics steps run with psi
@@ -488,11 +489,17 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
-    for (int k = 0; k < a.n_steps; ++k) {
+    int n_my = a.n_steps;
+    if (a.env_steps) {
+        const int e = a.env_steps[env];
+        n_my = e < 0 ? 0 : (e < n_my ? e : n_my);
+    }
+    n_my = __builtin_amdgcn_readfirstlane(n_my);
+    for (int k = 0; k < n_my; ++k) {
         if ((k & 63) == 0) {   // lane j: normals of step k + j
             if (a.noise) {
                 const int kk = k + lane;
-                if (kk < a.n_steps) {
+                if (kk < n_my) {
                     nz0 = a.noise[((size_t)kk * a.B + env) * 2];
                     nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
                 }
@@ -754,7 +761,8 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
     }
 }
 
-// what: 0 = x_expectation (double), 1 = outside probability (double), 2 = boundary Fail (int32)
+// what: 0 = x_expectation (double), 1 = outside probability (double), 2 = boundary Fail (int32),
+//       3 = energy Re<psi|H|psi> w at F = 0 (double), 4 = Fock phonon number sum n |psi_n|^2 (double)
 template <int FAM, int R>
 __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth, void* out) {
     const int lane = threadIdx.x & 63;
@@ -780,7 +788,7 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
             const int r = base + j;
             if (r >= c - w && r < c + w) s[0] += psi[j].re * psi[j].re + psi[j].im * psi[j].im;
         }
-    } else {
+    } else if (what == 2) {
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const int r = base + j;
@@ -788,10 +796,19 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
             if (r >= N - a.bnd_len && r < N) s[1] += p2;
             if (r < a.bnd_len) s[2] += p2;
         }
+    } else if (what == 3) {
+        cd hp[R], xx[R];
+        apply_hx<FAM, R>(psi, hp, xx, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[0] += psi[j].re * hp[j].re + psi[j].im * hp[j].im;
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[0] += (double)(base + j) * (psi[j].re * psi[j].re + psi[j].im * psi[j].im);
     }
     wave_sum<3>(s);
     if (lane == 0) {
-        if (what == 0) ((double*)out)[env] = s[0] * a.w;
+        if (what == 0 || what == 3) ((double*)out)[env] = s[0] * a.w;
+        else if (what == 4) ((double*)out)[env] = s[0];
         else if (what == 1) ((double*)out)[env] = 1.0 - s[0] * a.h;
         else {
             bool f = sqrt(s[1]) > a.fail_thr;
@@ -856,78 +873,35 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const ui
         }
 }
 
-// ---- dispatch ---------------------------------------------------------------------------------
-#define QC_FOR_EACH_R0(X) X(0, 1) X(0, 2) X(0, 4) X(0, 8)
-#define QC_FOR_EACH_R1(X) X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(1, 8) X(1, 16)
-#define QC_FOR_EACH_R2(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(2, 9) X(2, 17)
-#define QC_FOR_ALL(X) QC_FOR_EACH_R0(X) QC_FOR_EACH_R1(X) QC_FOR_EACH_R2(X)
+}  // namespace qcart
 
-static int fam_of(int family) { return family <= 1 ? family : 2; }
+namespace qcart {
 
 static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
-bool have_kernel(int family, int R) {
-    const int F = fam_of(family);
-#define QC_HAVE(FF, RR) \
-    if (F == FF && R == RR) return true;
-    QC_FOR_ALL(QC_HAVE)
-#undef QC_HAVE
-    return false;
+// per-family launch entry points, instantiated in qcart_k_{ho,iho,grid}.hip
+template <int FAM, int R>
+int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
+               double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
+               void* stream) {
+    const dim3 grid(nblocks(a.B)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (kind == 0) hipLaunchKernelGGL((k_step<FAM, R>), grid, block, 0, st, a);
+    else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R>), grid, block, 0, st, a);
+    else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R>), grid, block, 0, st, a, what, xth, out);
+    else hipLaunchKernelGGL((k_reset<FAM, R>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int launch_step(int family, int R, const KArgs& a, void* stream) {
-    const int F = fam_of(family);
-    if (a.B <= 0) return 0;
-#define QC_LAUNCH(FF, RR)                                                                              \
-    if (F == FF && R == RR) {                                                                          \
-        hipLaunchKernelGGL((k_step<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a); \
-        return hipGetLastError() == hipSuccess ? 0 : -3;                                               \
-    }
-    QC_FOR_ALL(QC_LAUNCH)
-#undef QC_LAUNCH
-    return -6;
-}
-
-int launch_obs(int family, int R, const KArgs& a, void* stream) {
-    const int F = fam_of(family);
-    if (a.B <= 0) return 0;
-#define QC_LAUNCH(FF, RR)                                                                             \
-    if (F == FF && R == RR) {                                                                         \
-        hipLaunchKernelGGL((k_obs<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a); \
-        return hipGetLastError() == hipSuccess ? 0 : -3;                                              \
-    }
-    QC_FOR_ALL(QC_LAUNCH)
-#undef QC_LAUNCH
-    return -6;
-}
-
-int launch_aux(int family, int R, int what, const KArgs& a, double xth, void* out, void* stream) {
-    const int F = fam_of(family);
-    if (a.B <= 0) return 0;
-#define QC_LAUNCH(FF, RR)                                                                                   \
-    if (F == FF && R == RR) {                                                                               \
-        hipLaunchKernelGGL((k_aux<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a, what, \
-                           xth, out);                                                                       \
-        return hipGetLastError() == hipSuccess ? 0 : -3;                                                    \
-    }
-    QC_FOR_ALL(QC_LAUNCH)
-#undef QC_LAUNCH
-    return -6;
-}
-
-int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mask, double a0, double a1,
-                 double a2, const double* k_arr, const double* m_arr, const double* s_arr, void* stream) {
-    const int F = fam_of(family);
-    if (a.B <= 0) return 0;
-#define QC_LAUNCH(FF, RR)                                                                                     \
-    if (F == FF && R == RR) {                                                                                 \
-        hipLaunchKernelGGL((k_reset<FF, RR>), dim3(nblocks(a.B)), dim3(256), 0, (hipStream_t)stream, a, kind, \
-                           mask, a0, a1, a2, k_arr, m_arr, s_arr);                                            \
-        return hipGetLastError() == hipSuccess ? 0 : -3;                                                      \
-    }
-    QC_FOR_ALL(QC_LAUNCH)
-#undef QC_LAUNCH
-    return -6;
-}
+// returns -6 when R is not instantiated for the family
+int launch_fam0(int R, int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
+                double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
+                void* stream);
+int launch_fam1(int R, int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
+                double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
+                void* stream);
+int launch_fam2(int R, int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
+                double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
+                void* stream);
 
 }  // namespace qcart

@@ -114,6 +114,8 @@ int qc_add_force(qc_handle* h, double force);
  *   psi       [B][N] complex128, advanced in place (the reference mutates `state` in place).
  *   actions   [B] int32 action index per env (0..n_actions-1 or a qc_add_force slot);
  *             NULL -> every env uses `default_action`.
+ *   env_steps [B] int32 per-env step budget: env e advances min(n_steps, env_steps[e]) steps (0 =
+ *             frozen, e.g. a finished episode awaiting reset); NULL -> n_steps for every env.
  *   noise     [n_steps][B][2] fp64 N(0,1) draws to inject (parity tests), or NULL for the
  *             in-kernel Philox4x32-10 stream keyed by (seed, env_offset + e, step counter).
  *   q_out, xmean_out  [n_steps][B] per-step (q, x_mean) outputs of step(), or NULL.
@@ -126,7 +128,7 @@ int qc_add_force(qc_handle* h, double force);
  * The step counter advances by n_steps.
  */
 int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_action, int32_t n_steps,
-            const double* noise, double* q_out, double* xmean_out, int32_t* fail_step,
+            const int32_t* env_steps, const double* noise, double* q_out, double* xmean_out, int32_t* fail_step,
             int32_t* term_step, double* obs_out);
 
 /* get_moments(state, out) (QO/simulation_quart.cpp:363-388) for grids; the Fock 'xp' vector
@@ -141,6 +143,13 @@ int qc_outside_prob(qc_handle* h, const void* psi, double xth, double* out);
 
 /* check_boundary_error (IHO/simulation_i.cpp:422-426, QO/simulation_quart.cpp:559-565): out [B] */
 int qc_boundary_fail(qc_handle* h, const void* psi, int32_t* out);
+
+/* cal_energy(state, Hamil) (QO/main_parallel.py:52-53, quartic reward) = Re<psi|H|psi> w with the
+ * force-free H: out [B] */
+int qc_energy(qc_handle* h, const void* psi, double* out);
+
+/* phonon_number(state) (HO/main_parallel.py:88-89, harmonic-cooling reward) = sum n |psi_n|^2: out [B] */
+int qc_phonon_number(qc_handle* h, const void* psi, double* out);
 
 /* Episode reset of psi for envs with mask[e] != 0 (mask NULL = all; device uint8 [B]):
  *   QC_RESET_GROUND   Fock |0> (IHO/main_parallel.py:231-232, HO/main_parallel.py:226-227)

@@ -48,13 +48,58 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// ---- cross-lane primitives (VALU only: DPP and v_permlane*_swap, no LDS round trip)
+// dst lane i <- src lane (i -/+ 1); a lane whose source is outside the wave reads 0 (bound_ctrl)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)(u & 0xffffffffull), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double shr1(double v) { return dpp_d<0x138>(v); }   // wave_shr:1
+__device__ __forceinline__ double shl1(double v) { return dpp_d<0x130>(v); }   // wave_shl:1
+template <int D>
+__device__ __forceinline__ double shr(double v) {
+    if constexpr (D == 0) return v;
+    else return shr<D - 1>(shr1(v));
+}
+template <int D>
+__device__ __forceinline__ double shl(double v) {
+    if constexpr (D == 0) return v;
+    else return shl<D - 1>(shl1(v));
+}
+__device__ __forceinline__ double mk_d(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// x + (x of the other half): v_permlane16_swap pairs rows (0,1),(2,3); v_permlane32_swap halves
+__device__ __forceinline__ double add_swap16(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const auto a = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+    return mk_d(a[0], b[0]) + mk_d(a[1], b[1]);
+}
+__device__ __forceinline__ double add_swap32(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const auto a = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+    return mk_d(a[0], b[0]) + mk_d(a[1], b[1]);
+}
+// all-lane sum; every pairing is symmetric, so every lane ends with bit-identical values
 template <int NV>
 __device__ __forceinline__ void wave_sum(double (&v)[NV]) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0xb1>(v[i]);    // quad_perm [1,0,3,2]
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], off, 64);
-    }
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x4e>(v[i]);    // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x141>(v[i]);   // row_half_mirror
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x140>(v[i]);   // row_mirror
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = add_swap16(v[i]);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = add_swap32(v[i]);
 }
 
 // ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
@@ -67,7 +112,9 @@ struct Fam<1> { static constexpr int KL = 2; };
 template <>
 struct Fam<2> { static constexpr int KL = 4; };
 
-// ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t
+// ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t.
+// Lanes outside the wave read 0 (the operators have zero rows there). dl is compile-time: the shift
+// by dl lanes is dl chained DPP wave shifts.
 template <int R, int H>
 __device__ __forceinline__ void make_ext(const cd (&v)[R], cd (&e)[R + 2 * H], int lane) {
 #pragma unroll
@@ -77,21 +124,23 @@ __device__ __forceinline__ void make_ext(const cd (&v)[R], cd (&e)[R + 2 * H], i
         const int o = H - t;
         const int dl = (o + R - 1) / R;
         const int idx = dl * R - o;
-        double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
-        const bool ok = lane >= dl;
-        e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+        if (dl == 1) e[t] = C(shr1(v[idx].re), shr1(v[idx].im));
+        else if (dl == 2) e[t] = C(shr<2>(v[idx].re), shr<2>(v[idx].im));
+        else if (dl == 3) e[t] = C(shr<3>(v[idx].re), shr<3>(v[idx].im));
+        else e[t] = C(shr<4>(v[idx].re), shr<4>(v[idx].im));
     }
 #pragma unroll
     for (int t = 0; t < H; ++t) {
         const int o = R + t;
         const int dl = o / R;
         const int idx = o - dl * R;
-        double re = __shfl_down(v[idx].re, dl, 64), im = __shfl_down(v[idx].im, dl, 64);
-        const bool ok = lane + dl < 64;
-        e[H + R + t] = C(ok ? re : 0.0, ok ? im : 0.0);
+        if (dl == 1) e[H + R + t] = C(shl1(v[idx].re), shl1(v[idx].im));
+        else if (dl == 2) e[H + R + t] = C(shl<2>(v[idx].re), shl<2>(v[idx].im));
+        else if (dl == 3) e[H + R + t] = C(shl<3>(v[idx].re), shl<3>(v[idx].im));
+        else e[H + R + t] = C(shl<4>(v[idx].re), shl<4>(v[idx].im));
     }
 }
-// lower halo only: e[t] = row base - H + t, t < H
+// lower halo only: e[t] = row base - H + t, t < H (up to 10 rows: dl <= 10 lanes for R = 1)
 template <int R, int H>
 __device__ __forceinline__ void make_lo(const cd (&v)[R], cd (&e)[H], int lane) {
 #pragma unroll
@@ -99,9 +148,16 @@ __device__ __forceinline__ void make_lo(const cd (&v)[R], cd (&e)[H], int lane) 
         const int o = H - t;
         const int dl = (o + R - 1) / R;
         const int idx = dl * R - o;
-        double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
-        const bool ok = lane >= dl;
-        e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+        if (dl <= 4) {
+            if (dl == 1) e[t] = C(shr1(v[idx].re), shr1(v[idx].im));
+            else if (dl == 2) e[t] = C(shr<2>(v[idx].re), shr<2>(v[idx].im));
+            else if (dl == 3) e[t] = C(shr<3>(v[idx].re), shr<3>(v[idx].im));
+            else e[t] = C(shr<4>(v[idx].re), shr<4>(v[idx].im));
+        } else {
+            double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
+            const bool ok = lane >= dl;
+            e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+        }
     }
 }
 
@@ -263,7 +319,9 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
         const int d = 1 << lvl;
         cd p[KL];
 #pragma unroll
-        for (int k = 0; k < KL; ++k) p[k] = C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
+        for (int k = 0; k < KL; ++k)
+            p[k] = (lvl == 0) ? C(shr1(s[k].re), shr1(s[k].im))
+                              : C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
         if (lane >= d) {
             const double* T = tf + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
 #pragma unroll
@@ -274,10 +332,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
     }
     // incoming state from lane - 1, pass 2
 #pragma unroll
-    for (int k = 0; k < KL; ++k) {
-        double re = __shfl_up(s[k].re, 1, 64), im = __shfl_up(s[k].im, 1, 64);
-        s[k] = (lane >= 1) ? C(re, im) : C(0.0, 0.0);
-    }
+    for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         cd y = b[j];
@@ -304,7 +359,9 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
         const int d = 1 << lvl;
         cd p[KL];
 #pragma unroll
-        for (int k = 0; k < KL; ++k) p[k] = C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
+        for (int k = 0; k < KL; ++k)
+            p[k] = (lvl == 0) ? C(shl1(s[k].re), shl1(s[k].im))
+                              : C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
         if (lane + d < 64) {
             const double* T = tb + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
 #pragma unroll
@@ -314,10 +371,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
         }
     }
 #pragma unroll
-    for (int k = 0; k < KL; ++k) {
-        double re = __shfl_down(s[k].re, 1, 64), im = __shfl_down(s[k].im, 1, 64);
-        s[k] = (lane + 1 < 64) ? C(re, im) : C(0.0, 0.0);
-    }
+    for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
         cd x = cmul(ld(dinv, base + j), b[j]);

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqcart.so")
+# QCART_LIB selects an alternative in-tree build (A/B experiments); default: the package's libqcart.so
+LIB_PATH = os.environ.get("QCART_LIB") or os.path.join(_HERE, "libqcart.so")
 
 QC_HO, QC_IHO, QC_QO, QC_IQO = 0, 1, 2, 3
 QC_A_REFERENCE, QC_A_EXACT = 0, 1

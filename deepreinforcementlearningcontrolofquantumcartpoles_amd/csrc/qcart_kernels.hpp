@@ -494,8 +494,11 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
+#ifndef QC_STEP_MIN_WAVES
+#define QC_STEP_MIN_WAVES 1   // waves per SIMD the step kernel's register budget must admit
+#endif
 template <int FAM, int R>
-__global__ __launch_bounds__(256) void k_step(const KArgs a) {
+__global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
     const int lane = threadIdx.x & 63;
     const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);

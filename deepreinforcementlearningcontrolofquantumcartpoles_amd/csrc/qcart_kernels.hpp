@@ -494,6 +494,11 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
+constexpr int kNoiseChunk = 256;   // physics steps of noise staged in LDS per wave
+
+#ifndef QC_RELOAD_TABLES
+#define QC_RELOAD_TABLES 1    // re-read factor tables every step (register budget), see k_step
+#endif
 #ifndef QC_STEP_MIN_WAVES
 #define QC_STEP_MIN_WAVES 1   // waves per SIMD the step kernel's register budget must admit
 #endif
@@ -512,12 +517,12 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     slot = __builtin_amdgcn_readfirstlane(slot);
     slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
     const double cF = a.c * a.force[slot];
-    const double* lc = a.lc + (size_t)slot * KL * Np * 2;
-    const double* uc = a.uc + (size_t)slot * KL * Np * 2;
-    const double* dinv = a.dinv + (size_t)slot * Np * 2;
-    const double* m2 = a.m2 + (size_t)slot * 10 * Np;
-    const double* tf = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
-    const double* tb = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const double* lc0 = a.lc + (size_t)slot * KL * Np * 2;
+    const double* uc0 = a.uc + (size_t)slot * KL * Np * 2;
+    const double* dinv0 = a.dinv + (size_t)slot * Np * 2;
+    const double* m20 = a.m2 + (size_t)slot * 10 * Np;
+    const double* tf0 = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const double* tb0 = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
     const int kf = a.kf[slot], kb = a.kb[slot];
 
     double* gpsi = a.psi + (size_t)env * N * 2;
@@ -544,7 +549,10 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     }
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
     const uint32_t genv = (uint32_t)(a.env_offset + env);
-    double nz0 = 0.0, nz1 = 0.0;
+    // per-wave noise staging: lane j draws the normals of steps k0 + j + 64 t of a 256-step chunk
+    // before the chunk starts (the Box-Muller temporaries never overlap the step's live vectors)
+    __shared__ double s_noise[4][kNoiseChunk][2];
+    double(*nz)[2] = s_noise[threadIdx.x >> 6];
 
     int n_my = a.n_steps;
     if (a.env_steps) {
@@ -553,18 +561,35 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     }
     n_my = __builtin_amdgcn_readfirstlane(n_my);
     for (int k = 0; k < n_my; ++k) {
-        if ((k & 63) == 0) {   // lane j: normals of step k + j
-            if (a.noise) {
-                const int kk = k + lane;
+        if ((k & (kNoiseChunk - 1)) == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+            for (int t = 0; t < kNoiseChunk / 64; ++t) {
+                const int kk = k + lane + 64 * t;
+                double r0 = 0.0, r1 = 0.0;
                 if (kk < n_my) {
-                    nz0 = a.noise[((size_t)kk * a.B + env) * 2];
-                    nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
+                    if (a.noise) {
+                        r0 = a.noise[((size_t)kk * a.B + env) * 2];
+                        r1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
+                    } else {
+                        normals(a.seed, genv, a.step0 + (uint64_t)kk, 0u, r0, r1);
+                    }
                 }
-            } else {
-                normals(a.seed, genv, a.step0 + (uint64_t)(k + lane), 0u, nz0, nz1);
+                nz[lane + 64 * t][0] = r0;
+                nz[lane + 64 * t][1] = r1;
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
-        const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
+        const double r0 = nz[k & (kNoiseChunk - 1)][0], r1 = nz[k & (kNoiseChunk - 1)][1];
+#if QC_RELOAD_TABLES
+        // keep the per-slot factor tables in L1/L2 instead of letting LICM pin them in registers
+        const double *lc = lc0, *uc = uc0, *dinv = dinv0, *m2 = m20, *tf = tf0, *tb = tb0;
+        asm volatile("" : "+s"(lc), "+s"(uc), "+s"(dinv), "+s"(m2), "+s"(tf), "+s"(tb));
+#else
+        const double *lc = lc0, *uc = uc0, *dinv = dinv0, *m2 = m20, *tf = tf0, *tb = tb0;
+#endif
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 / 1.7320508075688772);
         if (lane == 0) {

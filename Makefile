@@ -22,17 +22,6 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
-# A/B variant: step kernel forced to a 256-VGPR budget (2 waves per SIMD)
-$(PKG)/libqcart_w2.so: $(CSRC)/qcart_k_ho.hip $(CSRC)/qcart_k_iho.hip $(CSRC)/qcart_k_grid.hip $(CSRC)/qcart_dispatch.cpp $(CSRC)/qcart_api.cpp $(CSRC)/qcart_tables.cpp $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -DQC_STEP_MIN_WAVES=2 -shared -o $@ $(filter %.hip %.cpp,$^)
-
-# A/B variant: factor tables pinned in registers by LICM (the pre-reload behaviour)
-$(PKG)/libqcart_pin.so: $(CSRC)/qcart_k_ho.hip $(CSRC)/qcart_k_iho.hip $(CSRC)/qcart_k_grid.hip $(CSRC)/qcart_dispatch.cpp $(CSRC)/qcart_api.cpp $(CSRC)/qcart_tables.cpp $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -DQC_RELOAD_TABLES=0 -shared -o $@ $(filter %.hip %.cpp,$^)
-
-resource-usage:
-	python3 tools/kernel_resources.py $(CSRC)/build/qcart_k_*.o
-
 clean:
 	rm -rf $(CSRC)/build $(LIB)
 	$(MAKE) -C oracle clean

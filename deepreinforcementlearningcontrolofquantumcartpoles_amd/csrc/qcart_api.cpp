@@ -5,7 +5,9 @@
 // kernels of qcart_kernels.hip; there is no CPU fallback: a missing device or kernel is an error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -170,6 +172,19 @@ KArgs base_args(const qc_handle* h) {
         a.win_hi = c + w;
     }
     a.moment_order = op.fock ? 0 : p.moment_order;
+    {
+        int lf = 0, lb = 0;
+        for (auto& s : h->acts) {
+            lf = std::max(lf, s.kf);
+            lb = std::max(lb, s.kb);
+        }
+        a.lv_f = lf;
+        a.lv_b = lb;
+        const size_t bytes = (size_t)4 * (lf + lb) * op.kl * op.kl * kWave * 16;
+        // one 4-wave block per CU at the step kernel's register budget: up to 160 KiB of LDS
+        a.scan_lds = (op.fock && bytes <= 160 * 1024 && std::getenv("QCART_NO_SCAN_LDS") == nullptr) ? 1 : 0;
+        a.scan_lds_bytes = a.scan_lds ? (uint32_t)bytes : 0;
+    }
     a.n_obs = qc_n_obs(h);
     a.dt = p.dt;
     a.sqrt_dt = std::sqrt(p.dt);

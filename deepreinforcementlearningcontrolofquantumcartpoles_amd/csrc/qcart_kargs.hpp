@@ -29,7 +29,9 @@ struct KArgs {
     int32_t win_lo, win_hi;    // IQO outside-probability window [lo, hi); win_hi <= win_lo: off
     int32_t moment_order;
     int32_t n_obs;
-    int32_t pad0;
+    int32_t scan_lds;          // step kernel stages Kogge-Stone composites in LDS (Fock families)
+    int32_t lv_f, lv_b;        // max forward / backward scan levels over the slots (LDS image size)
+    uint32_t scan_lds_bytes;   // dynamic LDS per 4-wave block
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
     double a2, a3, a4, a5;     // Horner coefficients dt^3/12, dt^4/24, dt^5/80, dt^6/360

@@ -296,11 +296,19 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
 
 // ---- banded solve (zgbtrs, IHO/simulation_i.cpp:487, QO/simulation_quart.cpp:622) of the
 // precomputed pivot-free LU, in place on b.
-template <int KL, int R>
+// Composite T_lvl(lane) element e = i*KL + k: from global ([lvl][lane][e]) or, when the wave has
+// staged its own lane's composites in LDS, from the lane-private LDS image ([lvl][e][lane]).
+template <int KL, bool LDS>
+__device__ __forceinline__ cd comp(const double* g, const double* l, int lvl, int e, int lane) {
+    if constexpr (LDS) return ld(l, ((size_t)lvl * KL * KL + e) * 64 + lane);
+    else return ld(g, ((size_t)lvl * 64 + lane) * KL * KL + e);
+}
+
+template <int KL, int R, bool LDS>
 __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict__ lc, const double* __restrict__ uc,
                                            const double* __restrict__ dinv, const double* __restrict__ tf,
-                                           const double* __restrict__ tb, int kf, int kb, int lane, int base,
-                                           int Np) {
+                                           const double* __restrict__ tb, const double* ltf, const double* ltb,
+                                           int kf, int kb, int lane, int base, int Np) {
     // forward, pass 1 (zero incoming state): lane end state e_l
     cd s[KL];
 #pragma unroll
@@ -323,11 +331,10 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
             p[k] = (lvl == 0) ? C(shr1(s[k].re), shr1(s[k].im))
                               : C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
         if (lane >= d) {
-            const double* T = tf + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
 #pragma unroll
             for (int i = 0; i < KL; ++i)
 #pragma unroll
-                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], ld(T, i * KL + k), p[k]);
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], comp<KL, LDS>(tf, ltf, lvl, i * KL + k, lane), p[k]);
         }
     }
     // incoming state from lane - 1, pass 2
@@ -363,11 +370,10 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
             p[k] = (lvl == 0) ? C(shl1(s[k].re), shl1(s[k].im))
                               : C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
         if (lane + d < 64) {
-            const double* T = tb + ((size_t)(lvl * 64 + lane)) * KL * KL * 2;
 #pragma unroll
             for (int i = 0; i < KL; ++i)
 #pragma unroll
-                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], ld(T, i * KL + k), p[k]);
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], comp<KL, LDS>(tb, ltb, lvl, i * KL + k, lane), p[k]);
         }
     }
 #pragma unroll
@@ -494,16 +500,8 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
-constexpr int kNoiseChunk = 256;   // physics steps of noise staged in LDS per wave
-
-#ifndef QC_RELOAD_TABLES
-#define QC_RELOAD_TABLES 1    // re-read factor tables every step (register budget), see k_step
-#endif
-#ifndef QC_STEP_MIN_WAVES
-#define QC_STEP_MIN_WAVES 1   // waves per SIMD the step kernel's register budget must admit
-#endif
-template <int FAM, int R>
-__global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) {
+template <int FAM, int R, bool LDS>
+__global__ __launch_bounds__(256) void k_step(const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
     const int lane = threadIdx.x & 63;
     const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -517,13 +515,36 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     slot = __builtin_amdgcn_readfirstlane(slot);
     slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
     const double cF = a.c * a.force[slot];
-    const double* lc0 = a.lc + (size_t)slot * KL * Np * 2;
-    const double* uc0 = a.uc + (size_t)slot * KL * Np * 2;
-    const double* dinv0 = a.dinv + (size_t)slot * Np * 2;
-    const double* m20 = a.m2 + (size_t)slot * 10 * Np;
-    const double* tf0 = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
-    const double* tb0 = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const double* lc = a.lc + (size_t)slot * KL * Np * 2;
+    const double* uc = a.uc + (size_t)slot * KL * Np * 2;
+    const double* dinv = a.dinv + (size_t)slot * Np * 2;
+    const double* m2 = a.m2 + (size_t)slot * 10 * Np;
+    const double* tf = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const double* tb = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
     const int kf = a.kf[slot], kb = a.kb[slot];
+    // Stage this lane's own Kogge-Stone composites into a lane-private LDS image: the scan then
+    // reads them at LDS latency every step without pinning them in registers.
+    extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
+    double* ltf = smem_dyn + (size_t)(threadIdx.x >> 6) * (a.lv_f + a.lv_b) * KL * KL * 64 * 2;
+    double* ltb = ltf + (size_t)a.lv_f * KL * KL * 64 * 2;
+    if constexpr (LDS) {
+        for (int lvl = 0; lvl < kf; ++lvl)
+#pragma unroll
+            for (int e = 0; e < KL * KL; ++e) {
+                const cd v = ld(tf, ((size_t)lvl * 64 + lane) * KL * KL + e);
+                const size_t o = (((size_t)lvl * KL * KL + e) * 64 + lane) * 2;
+                ltf[o] = v.re;
+                ltf[o + 1] = v.im;
+            }
+        for (int lvl = 0; lvl < kb; ++lvl)
+#pragma unroll
+            for (int e = 0; e < KL * KL; ++e) {
+                const cd v = ld(tb, ((size_t)lvl * 64 + lane) * KL * KL + e);
+                const size_t o = (((size_t)lvl * KL * KL + e) * 64 + lane) * 2;
+                ltb[o] = v.re;
+                ltb[o + 1] = v.im;
+            }
+    }
 
     double* gpsi = a.psi + (size_t)env * N * 2;
     cd psi[R];
@@ -549,10 +570,7 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     }
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
     const uint32_t genv = (uint32_t)(a.env_offset + env);
-    // per-wave noise staging: lane j draws the normals of steps k0 + j + 64 t of a 256-step chunk
-    // before the chunk starts (the Box-Muller temporaries never overlap the step's live vectors)
-    __shared__ double s_noise[4][kNoiseChunk][2];
-    double(*nz)[2] = s_noise[threadIdx.x >> 6];
+    double nz0 = 0.0, nz1 = 0.0;
 
     int n_my = a.n_steps;
     if (a.env_steps) {
@@ -561,35 +579,18 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
     }
     n_my = __builtin_amdgcn_readfirstlane(n_my);
     for (int k = 0; k < n_my; ++k) {
-        if ((k & (kNoiseChunk - 1)) == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-            for (int t = 0; t < kNoiseChunk / 64; ++t) {
-                const int kk = k + lane + 64 * t;
-                double r0 = 0.0, r1 = 0.0;
+        if ((k & 63) == 0) {   // lane j: normals of step k + j
+            if (a.noise) {
+                const int kk = k + lane;
                 if (kk < n_my) {
-                    if (a.noise) {
-                        r0 = a.noise[((size_t)kk * a.B + env) * 2];
-                        r1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
-                    } else {
-                        normals(a.seed, genv, a.step0 + (uint64_t)kk, 0u, r0, r1);
-                    }
+                    nz0 = a.noise[((size_t)kk * a.B + env) * 2];
+                    nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
                 }
-                nz[lane + 64 * t][0] = r0;
-                nz[lane + 64 * t][1] = r1;
+            } else {
+                normals(a.seed, genv, a.step0 + (uint64_t)(k + lane), 0u, nz0, nz1);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
         }
-        const double r0 = nz[k & (kNoiseChunk - 1)][0], r1 = nz[k & (kNoiseChunk - 1)][1];
-#if QC_RELOAD_TABLES
-        // keep the per-slot factor tables in L1/L2 instead of letting LICM pin them in registers
-        const double *lc = lc0, *uc = uc0, *dinv = dinv0, *m2 = m20, *tf = tf0, *tb = tb0;
-        asm volatile("" : "+s"(lc), "+s"(uc), "+s"(dinv), "+s"(m2), "+s"(tf), "+s"(tb));
-#else
-        const double *lc = lc0, *uc = uc0, *dinv = dinv0, *m2 = m20, *tf = tf0, *tb = tb0;
-#endif
+        const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 / 1.7320508075688772);
         if (lane == 0) {
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(256, QC_STEP_MIN_WAVES) void k_step(const KArgs a) 
             }
         }
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R>(acc, lc, uc, dinv, tf, tb, kf, kb, lane, base, Np);
+        band_solve<KL, R, LDS>(acc, lc, uc, dinv, tf, tb, ltf, ltb, kf, kb, lane, base, Np);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
             cd xn[R];
@@ -968,7 +969,20 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
                void* stream) {
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 0) hipLaunchKernelGGL((k_step<FAM, R>), grid, block, 0, st, a);
+    if (kind == 0) {
+        if (FAM <= 1 && a.scan_lds) {
+            static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+            if (!attr_set) {
+                if (hipFuncSetAttribute((const void*)k_step<FAM, R, (FAM <= 1)>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                    return -3;
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((k_step<FAM, R, (FAM <= 1)>), grid, block, a.scan_lds_bytes, st, a);
+        }
+        else
+            hipLaunchKernelGGL((k_step<FAM, R, false>), grid, block, 0, st, a);
+    }
     else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R>), grid, block, 0, st, a);
     else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R>), grid, block, 0, st, a, what, xth, out);
     else hipLaunchKernelGGL((k_reset<FAM, R>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);

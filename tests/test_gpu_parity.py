@@ -119,7 +119,7 @@ def run_pair(oracle_mod, ph, steps, B, act_lo, act_hi, chunk=80, seed=7, policy=
 
 
 @pytest.mark.parametrize("name,steps,B,policy", [
-    ("iho64_g05", 1000, 8, "pd"), ("iho181", 1000, 8, "random"), ("iho512_g05", 1000, 8, "pd"),
+    ("iho64", 1000, 8, "random"), ("iho181", 1000, 8, "random"), ("iho512_g05", 1000, 8, "pd"),
     ("iho512", 1000, 8, "random"), ("iho512_exact_g05", 1000, 4, "pd"),
     ("ho256", 1000, 6, "random"), ("ho71", 1000, 8, "random"), ("qo171", 1000, 6, "random"),
     ("iqo513", 1000, 4, "random"),
@@ -310,3 +310,20 @@ def test_env_steps_budget_freezes_envs():
     st.step(ref, None, 80)
     assert torch.equal(a[0], ref[0]) and torch.equal(a[3], ref[3])
     assert not torch.equal(a[2], ref[2])
+
+
+def test_scan_composites_lds_and_global_paths_bitwise_equal(monkeypatch):
+    """The step kernel's LDS-staged Kogge-Stone composites give bit-identical results to the
+    global-memory path."""
+    ph = CASES["iho512"]
+    st = Stepper(ph, 8, 0, seed=11)
+    a = st.new_state()
+    st.reset(a, 1, arg0=16)
+    b = a.clone()
+    acts = torch.randint(0, 21, (8,), dtype=torch.int32, device="cuda")
+    st.step(a, acts, 80)
+    st.step_counter = 0
+    monkeypatch.setenv("QCART_NO_SCAN_LDS", "1")
+    st.step(b, acts, 80)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

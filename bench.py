@@ -73,6 +73,20 @@ def cpu_baseline(physics, seconds: float, threads: int):
                       f"one single-threaded env per thread), {dtm:.1f} s wall"}
 
 
+def latest_profile(workload: str):
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        bl = d.get("bench_line") or {}
+        if bl.get("config", {}).get("workload") == workload and "hbm_bytes_per_launch" in d:
+            best = d
+    return best
+
+
 def main():
     args = parse()
     import torch
@@ -170,6 +184,13 @@ def main():
         "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": PEAK_FP64_VALU / 1e12,
                  "frac": flops / PEAK_FP64_VALU, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
     }
+    # HBM traffic per launch measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, tools/prof_summary.py)
+    # for this same workload, when a committed profile exists
+    prof = latest_profile(res["config"]["workload"])
+    if prof is not None:
+        res["roofline"]["traffic"] = prof["hbm_bytes_per_launch"]
+        res["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC, profiles/%s_summary.json)" % prof["tag"]
+        res["roofline"]["algorithmic_bytes_per_launch"] = 32.0 * N * per_launch_units
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(ph, args.cpu_seconds, args.cpu_threads)

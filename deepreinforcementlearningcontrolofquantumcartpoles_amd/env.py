@@ -1,0 +1,191 @@
+"""BatchedEnv: the reference actors' episode loop (Control.do_episode) for B environments at once,
+on device tensors, one control interval per step().
+
+Reference semantics reproduced per family ('xp' observation input):
+  * cartpoles (IHO, IQO): IHO/main_parallel.py:227-268, IQO/main_parallel.py:172-222
+      - reset: IHO |0>, IQO Gaussian_packet(inf, 0, 1); force 0 for the first control interval
+        (no control at the zero-th step), first decision at i = control_interval
+      - done when the boundary Fail flag fired during the interval (numerical_failure) or, at the
+        control step, |<x>| > xth = F_max (IHO) / the outside probability exceeded 0.5 at any
+        physics step (IQO, checked every step); reward row value 1 (alive) or failing_reward (-1)
+  * cooling (HO, QO): HO/main_parallel.py:224-260, QO/main_parallel.py:169-232
+      - reset: HO |0>; QO Gaussian(k ~ U[-0.3,0.3]) evolved U[15,20] time units at F = 0, redrawn
+        until energy < 7.5 and no Fail (QO/main_parallel.py:177-198)
+      - first decision at i = 0; at each control step the transition is stored with reward
+        -phonon*scale (HO) / -energy*scale (QO) while phonon <= cutoff / energy < cutoff and no Fail;
+        otherwise the episode ends without storing it; the episode is truncated at t_max = 100
+The experience row layout is the reference's: [last_obs, obs, last_action, reward]
+(IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import config as cfg
+from .core import Stepper
+
+
+class BatchedEnv:
+    def __init__(self, physics: cfg.Physics, batch: int, device: int | str | torch.device = 0, seed: int = 0,
+                 env_offset: int = 0, input_scaling: float = 1.0, failing_reward: float = -1.0,
+                 reward_multiply: float = 1.0, t_max: float = 100.0, phonon_cutoff: float = 20.0,
+                 energy_cutoff: float = 12.0, init_energy_cutoff: float = 7.5, auto_reset: bool = True,
+                 reset_kind: str = "reference"):
+        self.ph = physics
+        self.B = int(batch)
+        self.st = Stepper(physics, self.B, device, seed=seed, env_offset=env_offset)
+        self.dev = self.st.device
+        self.psi = self.st.new_state()
+        self.ci = physics.control_interval
+        self.half = physics.n_actions // 2
+        self.input_scaling = input_scaling
+        self.failing_reward = failing_reward
+        self.reward_multiply = reward_multiply
+        self.t_max = t_max
+        self.phonon_cutoff = phonon_cutoff
+        self.energy_cutoff = energy_cutoff
+        self.init_energy_cutoff = init_energy_cutoff
+        self.auto_reset = auto_reset
+        self.reset_kind = reset_kind
+        self.cartpole = physics.family in (cfg.IHO, cfg.IQO)
+        self.gen = torch.Generator(device=self.dev).manual_seed(int(seed) * 7919 + int(env_offset))
+        z = lambda dt: torch.zeros(self.B, dtype=dt, device=self.dev)  # noqa: E731
+        self.t = z(torch.float64)                 # episode time
+        self.steps = z(torch.int64)               # physics steps in the episode
+        self.last_action = torch.full((self.B,), self.half, dtype=torch.int32, device=self.dev)
+        self.obs = torch.zeros((self.B, self.st.n_obs), dtype=torch.float32, device=self.dev)
+        self.episode_return = z(torch.float64)
+        self.finished_returns: list = []          # (return, length) of finished episodes (host)
+
+    # ------------------------------------------------------------------ observation
+    def _observe(self) -> torch.Tensor:
+        return self.st.moments(self.psi).to(torch.float32) * self.input_scaling
+
+    def _quantity(self) -> torch.Tensor:
+        """cooling reward quantity: phonon number (HO) / energy (QO)."""
+        if self.ph.family == cfg.HO:
+            return self.st.phonon_number(self.psi)
+        return self.st.energy(self.psi)
+
+    # ------------------------------------------------------------------ reset
+    def _reset_states(self, mask: torch.Tensor):
+        m8 = mask.to(torch.uint8)
+        fam = self.ph.family
+        if fam in (cfg.HO, cfg.IHO):
+            if self.reset_kind == "synthetic":
+                self.st.reset(self.psi, 1, mask=m8, arg0=16)
+            else:
+                self.st.reset(self.psi, 0, mask=m8)
+        elif fam == cfg.IQO:
+            self.st.reset(self.psi, 2, mask=m8, arg0=0.0, arg1=0.0, arg2=1.0)
+        else:
+            self._reset_quartic_cooling(mask)
+
+    def _reset_quartic_cooling(self, mask: torch.Tensor):
+        """QO/main_parallel.py:177-198: random-k packet, free evolution for U[15,20] time units, redrawn
+        until energy < init_energy_cutoff and no Fail."""
+        todo = mask.clone()
+        dt = self.ph.dt
+        while bool(todo.any()):
+            k = (torch.rand(self.B, generator=self.gen, device=self.dev, dtype=torch.float64) * 0.6 - 0.3)
+            mu = torch.zeros(self.B, dtype=torch.float64, device=self.dev)
+            sg = torch.ones(self.B, dtype=torch.float64, device=self.dev)
+            self.st.reset(self.psi, 2, mask=todo.to(torch.uint8), k=k, mean=mu, std=sg)
+            init_t = torch.rand(self.B, generator=self.gen, device=self.dev, dtype=torch.float64) * 5.0 + 15.0
+            budget = torch.where(todo, torch.ceil(init_t / dt).to(torch.int32), torch.zeros_like(init_t, dtype=torch.int32))
+            failed = torch.zeros(self.B, dtype=torch.bool, device=self.dev)
+            chunk = 1440
+            while bool((budget > 0).any()):
+                out = self.st.step(self.psi, None, chunk, default_action=self.half,
+                                   env_steps=torch.clamp(budget, max=chunk).to(torch.int32))
+                failed |= out["fail_step"] > 0
+                budget = torch.clamp(budget - chunk, min=0)
+            ok = (self._quantity() < self.init_energy_cutoff) & ~failed
+            todo = todo & ~ok
+
+    def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Start new episodes (all, or where mask); returns the observation at the first decision."""
+        if mask is None:
+            mask = torch.ones(self.B, dtype=torch.bool, device=self.dev)
+        mask = mask.to(device=self.dev, dtype=torch.bool)
+        self._reset_states(mask)
+        self.t = torch.where(mask, torch.zeros_like(self.t), self.t)
+        self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
+        self.episode_return = torch.where(mask, torch.zeros_like(self.episode_return), self.episode_return)
+        self.last_action = torch.where(mask, torch.full_like(self.last_action, self.half), self.last_action)
+        if self.cartpole:
+            # no control at the zero-th step: one zero-force interval first (IHO:242-268, IQO:190-221).
+            # An episode that already ends at i = control_interval stores nothing (i != control_interval
+            # guard, IHO:250) and is simply restarted here.
+            todo = mask.clone()
+            while bool(todo.any()):
+                budget = torch.where(todo, torch.full_like(self.last_action, self.ci), torch.zeros_like(self.last_action))
+                out = self.st.step(self.psi, None, self.ci, default_action=self.half, env_steps=budget,
+                                   want_term=(self.ph.family == cfg.IQO), want_obs=True)
+                bad = out["fail_step"] > 0
+                if self.ph.family == cfg.IQO:
+                    bad |= out["term_step"] >= 0
+                else:
+                    bad |= out["obs"][:, 0].abs() > self.ph.xth
+                bad &= todo
+                if bool(bad.any()):
+                    self._reset_states(bad)
+                todo = bad
+            self.t = torch.where(mask, self.t + self.ci * self.ph.dt, self.t)
+            self.steps = torch.where(mask, self.steps + self.ci, self.steps)
+        obs = self._observe()
+        self.obs = torch.where(mask[:, None], obs, self.obs)
+        return self.obs
+
+    # ------------------------------------------------------------------ step
+    def step(self, actions: torch.Tensor):
+        """Apply per-env actions for one control interval. Returns (obs, reward, done, info):
+        reward is the reference's stored reward-row value, info['valid'] marks transitions the
+        reference would store, info['numerical_failure'] the Fail-terminated episodes."""
+        actions = actions.to(device=self.dev, dtype=torch.int32).contiguous()
+        last_obs = self.obs
+        fam = self.ph.family
+        out = self.st.step(self.psi, actions, self.ci, want_fail=True, want_obs=True,
+                           want_term=(fam == cfg.IQO))
+        fail = out["fail_step"] > 0
+        obs = out["obs"].to(torch.float32) * self.input_scaling
+        self.t = self.t + self.ci * self.ph.dt
+        self.steps = self.steps + self.ci
+        if self.cartpole:
+            numerical = fail                                     # Fail during the interval (IHO:243-267)
+            if fam == cfg.IHO:
+                out_of_bounds = out["obs"][:, 0].abs() > self.ph.xth   # |x_expectation| > xth (IHO:246)
+            else:
+                out_of_bounds = out["term_step"] >= 0                 # outside prob > 0.5 (IQO:199-200)
+            done = numerical | out_of_bounds
+            reward = torch.where(done, torch.full_like(self.t, self.failing_reward), torch.ones_like(self.t))
+            valid = torch.ones_like(done)
+        else:
+            q = self._quantity()
+            cutoff = self.phonon_cutoff if fam == cfg.HO else self.energy_cutoff
+            ok = (q <= cutoff) if fam == cfg.HO else (q < cutoff)
+            truncated = self.t >= self.t_max - 0.01 * self.ph.dt
+            done = fail | ~ok | truncated
+            reward = -q * self.reward_multiply
+            valid = ~done
+            numerical = fail
+        self.episode_return = self.episode_return + torch.where(valid, reward, torch.zeros_like(reward))
+        info = {"valid": valid, "numerical_failure": numerical & done, "t": self.t.clone(),
+                "last_obs": last_obs, "fail_step": out["fail_step"]}
+        self.last_action = actions
+        self.obs = obs
+        if bool(done.any()):
+            info["terminal_obs"] = obs.clone()
+            info["episode_return"] = self.episode_return.clone()
+            info["episode_length"] = self.t.clone()
+            self.finished_returns.append((self.episode_return[done].cpu(), self.t[done].cpu()))
+            if self.auto_reset:
+                self.reset(done)
+        return self.obs, reward.to(torch.float32), done, info
+
+    @staticmethod
+    def experience(last_obs: torch.Tensor, obs: torch.Tensor, action: torch.Tensor, reward: torch.Tensor):
+        """Experience rows in the reference layout np.hstack((last_data, data, [last_action], [reward]))."""
+        return torch.cat([last_obs, obs, action.to(torch.float32)[:, None], reward.to(torch.float32)[:, None]], 1)

@@ -1,0 +1,160 @@
+"""Drop-in surface of the reference CPython extension `simulation` (one env, numpy state).
+
+The reference builds one extension per physical system with compile-time macros (*/setupC.py) and
+the drivers call (IHO/main_parallel.py:174-264, IQO/main_parallel.py:123-218):
+
+    simulation = __import__('simulation')
+    simulation.set_seed(seed)
+    q, x_mean, Fail = simulation.step(state, time_step, force, gamma)   # state mutated in place
+    simulation.x_expectation(state); simulation.get_moments(state, data); simulation.check_settings()
+
+Here the compile-time parameters become arguments of `load()`, which returns a module-like object
+with the same function names, signatures, return values and error behaviour; each call runs the HIP
+kernels of libqcart (B = 1) and copies the numpy state to and from the device. This surface exists
+for drop-in compatibility; the throughput path is core.Stepper / env.BatchedEnv.
+
+Differences that cannot be pinned (documented in DESIGN.md): the noise is the counter-based Philox
+stream keyed by (seed, env 0, step) instead of MKL's MT19937.
+"""
+from __future__ import annotations
+
+import sys
+import types
+from math import pi
+
+import numpy as np
+
+from . import config as cfg
+
+_MODULES: dict = {}
+
+
+def _check_state(state, N):
+    if not isinstance(state, np.ndarray):
+        raise TypeError("The input object cannot be identified as a Numpy array")
+    if state.ndim != 1:
+        raise ValueError("The input array is not one-dimensional")
+    if state.shape[0] != N:
+        raise ValueError("The input array does not match the required size " + str(N))
+    if state.dtype != np.complex128:
+        raise ValueError("The input array does not match the required datatype: Complex128")
+
+
+class _Simulation:
+    """One compiled-parameter set of the reference module (see load())."""
+
+    def __init__(self, physics: cfg.Physics, device: int = 0):
+        import torch
+
+        from .core import Stepper
+        self._torch = torch
+        self.physics = physics
+        self._st = Stepper(physics, 1, device, seed=0)
+        self._dev = self._st.device
+        self._psi = self._st.new_state()
+        self._dt, self._gamma = physics.dt, physics.gamma
+        self.N = self._st.N
+
+    # set_seed(int): IHO/simulation_i.cpp:574-579
+    def set_seed(self, seed):
+        if not isinstance(seed, (int, np.integer)):
+            raise TypeError("seed must be an int")
+        self._st.set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
+        return None
+
+    # check_settings(): IHO/simulation_i.cpp:581-583 -> (n_max, omega); QO:652-654 -> (x_n, h, lambda, mass, moment)
+    def check_settings(self):
+        p = self.physics
+        if p.fock:
+            return (p.n_max, p.omega)
+        return (self.N, p.grid_size, p.lambda_, p.mass, p.moment_order)
+
+    def _sync_dynamics(self, dt, gamma):
+        if dt != self._dt or gamma != self._gamma:
+            self._st.set_dynamics(float(dt), float(gamma))
+            self._dt, self._gamma = dt, gamma
+
+    def _slot(self, force):
+        p = self.physics
+        half = p.n_actions // 2
+        spacing = p.f_max / half
+        a = round(force / spacing)
+        if -half <= a <= half and (a * spacing) == force:
+            return a + half
+        return self._st.add_force(float(force))
+
+    def _run(self, state, dt, force, gamma, n):
+        _check_state(state, self.N)
+        self._sync_dynamics(float(dt), float(gamma))
+        torch = self._torch
+        self._psi.copy_(torch.from_numpy(state).view(1, -1))
+        out = self._st.step(self._psi, None, n, default_action=self._slot(float(force)), want_q=True,
+                            want_fail=True)
+        state[:] = self._psi.view(-1).cpu().numpy()
+        return out
+
+    # step(state, dt, force, gamma) -> (q, x_mean, Fail): IHO/simulation_i.cpp:358-389
+    def step(self, state, dt, force, gamma):
+        out = self._run(state, dt, force, gamma, 1)
+        q = float(out["q"][0, 0])
+        xm = float(out["x_mean"][0, 0])
+        return q, xm, int(out["fail_step"][0] > 0)
+
+    # simulate_10_steps: IHO/simulation_i.cpp:391-421 (last step's q, x_mean; Fail of the final state)
+    def simulate_10_steps(self, state, dt, force, gamma):
+        out = self._run(state, dt, force, gamma, 10)
+        fail = int(self._st.boundary_fail(self._psi)[0])
+        return float(out["q"][9, 0]), float(out["x_mean"][9, 0]), fail
+
+    # x_expectation(state): IHO/simulation_i.cpp:204-215, QO/simulation_quart.cpp:244-258
+    def x_expectation(self, state):
+        _check_state(state, self.N)
+        self._psi.copy_(self._torch.from_numpy(state).view(1, -1))
+        return float(self._st.x_expectation(self._psi)[0])
+
+    # get_moments(state, data): QO/simulation_quart.cpp:363-388 (grid families only in the reference)
+    def get_moments(self, state, data):
+        _check_state(state, self.N)
+        n = self._st.n_obs
+        if not isinstance(data, np.ndarray) or data.ndim != 1:
+            raise ValueError("The moment data array is not one-dimensional")
+        if data.shape[0] != n:
+            raise ValueError("The moment data array does not match the required size " + str(n))
+        if data.dtype != np.float64:
+            raise ValueError("The moment data array does not match the required datatype: Float64")
+        self._psi.copy_(self._torch.from_numpy(state).view(1, -1))
+        data[:] = self._st.moments(self._psi)[0].cpu().numpy()
+        return None
+
+
+def load(family: int | str = cfg.IHO, device: int = 0, **params) -> types.ModuleType:
+    """Return a module-like object equivalent to the reference's compiled `simulation` extension.
+
+    family: 0/'harmonic', 1/'inverted_harmonic', 2/'quartic', 3/'inverted_quartic'; params are the
+    setupC.py macros (n_max, omega / x_max, grid_size, lambda_, mass, moment_order) and optionally
+    gamma, time_steps, f_max, a_mode (defaults: the drivers' values, config.DEFAULTS)."""
+    if isinstance(family, str):
+        family = {v: k for k, v in cfg.FAMILY_NAMES.items()}[family]
+    phys = cfg.DEFAULTS[family].with_(**params)
+    key = (device, tuple(sorted(phys.asdict().items())))
+    if key not in _MODULES:
+        sim = _Simulation(phys, device)
+        mod = types.ModuleType("simulation", "MI355X-native drop-in for the reference `simulation` module")
+        for name in ("step", "simulate_10_steps", "set_seed", "check_settings", "x_expectation"):
+            setattr(mod, name, getattr(sim, name))
+        if not phys.fock:
+            mod.get_moments = sim.get_moments
+        mod._impl = sim
+        _MODULES[key] = mod
+    return _MODULES[key]
+
+
+def install(family: int | str = cfg.IHO, device: int = 0, **params) -> types.ModuleType:
+    """Register the drop-in as `simulation` in sys.modules, so the reference drivers'
+    `__import__('simulation')` resolves to it."""
+    mod = load(family, device, **params)
+    sys.modules["simulation"] = mod
+    return mod
+
+
+__all__ = ["load", "install", "pi"]

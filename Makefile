@@ -4,7 +4,7 @@ PKG := deepreinforcementlearningcontrolofquantumcartpoles_amd
 CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
-OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_dispatch.o qcart_api.o qcart_tables.o)
+OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_group.o qcart_dispatch.o qcart_api.o qcart_tables.o)
 HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
 all: $(LIB) oracle
@@ -27,3 +27,11 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean resource-usage
+
+# experiment builds (not shipped): make expt EXPT=-DQCART_EXPT_NOLOAD NAME=noload
+EXPT ?=
+NAME ?= expt
+expt:
+	@mkdir -p $(CSRC)/build_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(EXPT) -c $(CSRC)/qcart_k_iho.hip -o $(CSRC)/build_$(NAME)/qcart_k_iho.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/qcart_k_iho.o $(filter-out $(CSRC)/build/qcart_k_iho.o,$(OBJS))

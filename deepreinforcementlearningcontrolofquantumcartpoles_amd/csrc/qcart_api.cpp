@@ -42,8 +42,10 @@ struct qc_handle {
     std::string err;
     // device buffers
     double *d_xu = nullptr, *d_xg = nullptr, *d_hu = nullptr;
-    double *d_lc = nullptr, *d_uc = nullptr, *d_dinv = nullptr, *d_m2 = nullptr;
-    double *d_tf = nullptr, *d_tb = nullptr, *d_force = nullptr;
+    double *d_tab = nullptr, *d_force = nullptr;
+    uint32_t slot_bytes = 0;
+    int32_t* d_order = nullptr;   // envs grouped by force slot (step kernel with per-block LDS tables)
+    size_t order_cap = 0;
     int32_t *d_kf = nullptr, *d_kb = nullptr;
 };
 
@@ -85,11 +87,12 @@ int pick_R(int family, int N) {
 }
 
 void free_dev(qc_handle* h) {
-    double** dp[] = {&h->d_xu, &h->d_xg, &h->d_hu, &h->d_lc, &h->d_uc, &h->d_dinv, &h->d_m2, &h->d_tf, &h->d_tb,
+    double** dp[] = {&h->d_xu, &h->d_xg, &h->d_hu, &h->d_tab,
                      &h->d_force};
     for (auto p : dp)
         if (*p) { (void)hipFree(*p); *p = nullptr; }
     if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
+    if (h->d_order) { (void)hipFree(h->d_order); h->d_order = nullptr; h->order_cap = 0; }
     if (h->d_kb) { (void)hipFree(h->d_kb); h->d_kb = nullptr; }
 }
 
@@ -102,35 +105,47 @@ int upload(qc_handle* h, T** dst, const T* src, size_t n) {
     return hip_check(h, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
 }
 
-// (re)build every slot's tables on the host and upload them (slot capacity kMaxSlots)
+// (re)build every slot's factor block on the host (SlotLayout, lane-interleaved) and upload them
+// (slot capacity kMaxSlots)
 int upload_tables(qc_handle* h) {
-    const int Np = h->op.Npad, kl = h->op.kl;
-    const size_t n_lc = (size_t)kMaxSlots * kl * Np * 2;
-    const size_t n_di = (size_t)kMaxSlots * Np * 2;
-    const size_t n_m2 = (size_t)kMaxSlots * kMirrorBands * Np;
-    const size_t blk = (size_t)kMaxLevels * kWave * kl * kl * 2;
-    std::vector<double> lc(n_lc, 0.0), uc(n_lc, 0.0), di(n_di, 0.0), m2(n_m2, 0.0);
-    std::vector<double> tf((size_t)kMaxSlots * blk, 0.0), tb((size_t)kMaxSlots * blk, 0.0), force(kMaxSlots, 0.0);
+    const int Np = h->op.Npad, kl = h->op.kl, R = h->op.R;
+    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO);
+    h->slot_bytes = L.bytes;
+    const size_t sd = L.bytes / 8;   // doubles per slot
+    std::vector<double> tab((size_t)kMaxSlots * sd, 0.0), force(kMaxSlots, 0.0);
     std::vector<int32_t> kf(kMaxSlots, 0), kb(kMaxSlots, 0);
+    auto ilv = [&](int b, int r) { return ((size_t)b * R + (r % R)) * kWave + r / R; };   // row-band element
+    auto put = [&](double* base, uint32_t off, size_t elem, cplx v) {
+        double* q = base + off / 8 + elem * 2;
+        q[0] = v.real();
+        q[1] = v.imag();
+    };
     for (size_t s = 0; s < h->acts.size(); s++) {
         const ActHost& a = h->acts[s];
-        std::memcpy(&lc[s * kl * Np * 2], a.lc.data(), sizeof(double) * kl * Np * 2);
-        std::memcpy(&uc[s * kl * Np * 2], a.uc.data(), sizeof(double) * kl * Np * 2);
-        std::memcpy(&di[s * Np * 2], a.dinv.data(), sizeof(double) * Np * 2);
-        std::memcpy(&m2[s * kMirrorBands * Np], a.m2.data(), sizeof(double) * kMirrorBands * Np);
-        std::memcpy(&tf[s * blk], a.tf.data(), sizeof(double) * blk);
-        std::memcpy(&tb[s * blk], a.tb.data(), sizeof(double) * blk);
+        double* blk = tab.data() + s * sd;
+        for (int b = 0; b < kl; b++)
+            for (int r = 0; r < Np; r++) {
+                put(blk, L.lc, ilv(b, r), a.lc[(size_t)b * Np + r]);
+                put(blk, L.uc, ilv(b, r), a.uc[(size_t)b * Np + r]);
+            }
+        for (int r = 0; r < Np; r++) put(blk, L.di, ilv(0, r), a.dinv[r]);
+        if (h->op.family == QC_IHO)
+            for (int b = 0; b < kMirrorBands; b++)
+                for (int r = 0; r < Np; r++) blk[L.m2 / 8 + ilv(b, r)] = a.m2[(size_t)b * Np + r];
+        const size_t kk = (size_t)kl * kl;
+        for (int v = 0; v < kTabLevels; v++)
+            for (int l = 0; l < kWave; l++)
+                for (size_t e = 0; e < kk; e++) {
+                    const size_t src = ((size_t)v * kWave + l) * kk + e, dst = ((size_t)v * kk + e) * kWave + l;
+                    put(blk, L.tf, dst, a.tf[src]);
+                    put(blk, L.tb, dst, a.tb[src]);
+                }
         force[s] = a.force;
         kf[s] = a.kf;
         kb[s] = a.kb;
     }
     int rc;
-    if ((rc = upload(h, &h->d_lc, lc.data(), lc.size()))) return rc;
-    if ((rc = upload(h, &h->d_uc, uc.data(), uc.size()))) return rc;
-    if ((rc = upload(h, &h->d_dinv, di.data(), di.size()))) return rc;
-    if ((rc = upload(h, &h->d_m2, m2.data(), m2.size()))) return rc;
-    if ((rc = upload(h, &h->d_tf, tf.data(), tf.size()))) return rc;
-    if ((rc = upload(h, &h->d_tb, tb.data(), tb.size()))) return rc;
+    if ((rc = upload(h, &h->d_tab, tab.data(), tab.size()))) return rc;
     if ((rc = upload(h, &h->d_force, force.data(), force.size()))) return rc;
     if ((rc = upload(h, &h->d_kf, kf.data(), kf.size()))) return rc;
     if ((rc = upload(h, &h->d_kb, kb.data(), kb.size()))) return rc;
@@ -173,18 +188,22 @@ KArgs base_args(const qc_handle* h) {
     }
     a.moment_order = op.fock ? 0 : p.moment_order;
     {
+        // step-kernel table placement: the slot block's lc/uc/di/m2 (and the kept scan composites) in
+        // the workgroup's LDS when they fit the 160 KiB of a CU (QCART_TAB_MODE overrides, for A/B)
         int lf = 0, lb = 0;
         for (auto& s : h->acts) {
             lf = std::max(lf, s.kf);
             lb = std::max(lb, s.kb);
         }
-        a.lv_f = lf;
-        a.lv_b = lb;
-        const size_t bytes = (size_t)4 * (lf + lb) * op.kl * op.kl * kWave * 16;
-        // one 4-wave block per CU at the step kernel's register budget: up to 160 KiB of LDS
-        a.scan_lds = (op.fock && bytes <= 160 * 1024 && std::getenv("QCART_NO_SCAN_LDS") == nullptr) ? 1 : 0;
-        a.scan_lds_bytes = a.scan_lds ? (uint32_t)bytes : 0;
+        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO);
+        const size_t t1 = L.tf, t2 = L.tf + (size_t)(lf + lb + 2) * op.kl * op.kl * 1024;
+        int mode = t2 <= 160 * 1024 ? 2 : (t1 <= 160 * 1024 ? 1 : 0);
+        if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
+        a.tab_mode = mode;
+        a.lds_bytes = (uint32_t)(mode == 2 ? t2 : (mode == 1 ? t1 : 0));
     }
+    a.order = nullptr;
+    a.n_blocks = (uint32_t)((p.batch + 3) / 4);
     a.n_obs = qc_n_obs(h);
     a.dt = p.dt;
     a.sqrt_dt = std::sqrt(p.dt);
@@ -207,12 +226,8 @@ KArgs base_args(const qc_handle* h) {
     a.xu = h->d_xu;
     a.xg = h->d_xg;
     a.hu = h->d_hu;
-    a.lc = h->d_lc;
-    a.uc = h->d_uc;
-    a.dinv = h->d_dinv;
-    a.m2 = h->d_m2;
-    a.tf = h->d_tf;
-    a.tb = h->d_tb;
+    a.tab = h->d_tab;
+    a.slot_bytes = h->slot_bytes;
     a.kf = h->d_kf;
     a.kb = h->d_kb;
     a.force = h->d_force;
@@ -400,6 +415,24 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.term_step = term_step;
     a.obs_out = obs_out;
     DeviceGuard g(h->device);
+    if (h->p.batch == 0) return QC_OK;
+    if (actions) {
+        // group envs by force slot, padded to whole 4-env blocks: every block then shares one slot's
+        // tables (the per-block LDS image); order within a slot does not change any result
+        const size_t cap = (size_t)((h->p.batch + 3) / 4) * 4 + 4 * (size_t)kMaxSlots;
+        if (h->order_cap < cap) {
+            if (h->d_order) (void)hipFree(h->d_order);
+            h->d_order = nullptr;
+            h->order_cap = 0;
+            hipError_t e = hipMalloc((void**)&h->d_order, cap * sizeof(int32_t));
+            if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+            h->order_cap = cap;
+        }
+        if (launch_group(actions, h->p.batch, (int)h->acts.size(), h->d_order, (int32_t)cap, h->stream))
+            return fail(h, QC_EHIP, "group kernel launch failed");
+        a.order = h->d_order;
+        a.n_blocks = (uint32_t)(cap / 4);
+    }
     int rc = launch_step(h->p.family, h->R, a, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
     h->step += (uint64_t)n_steps;

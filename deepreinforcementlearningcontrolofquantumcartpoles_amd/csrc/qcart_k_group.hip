@@ -1,0 +1,54 @@
+// qcart_k_group.hip — groups the envs of a step call by force slot so that each 4-wave workgroup of
+// the step kernel shares one slot's factor tables through LDS. One workgroup: LDS histogram of the
+// slots, 4-aligned group offsets, then a scatter of env ids (order inside a group is arbitrary and
+// does not affect any result: envs are independent). Unused entries are -1 (idle waves).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qcart_kargs.hpp"
+
+namespace qcart {
+
+constexpr int kGroupSlots = 64;
+
+__global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ actions, int64_t B, int n_slots,
+                                                int32_t* __restrict__ order, int32_t cap) {
+    __shared__ int cnt[kGroupSlots], off[kGroupSlots], cur[kGroupSlots];
+    __shared__ int total;
+    const int t = threadIdx.x;
+    if (t < kGroupSlots) {
+        cnt[t] = 0;
+        cur[t] = 0;
+    }
+    __syncthreads();
+    auto slot_of = [&](int64_t e) {
+        const int s = actions[e];
+        return s < 0 ? 0 : (s >= n_slots ? n_slots - 1 : s);
+    };
+    for (int64_t e = t; e < B; e += blockDim.x) atomicAdd(&cnt[slot_of(e)], 1);
+    __syncthreads();
+    if (t == 0) {
+        int o = 0;
+        for (int s = 0; s < kGroupSlots; ++s) {
+            off[s] = o;
+            o += (cnt[s] + 3) & ~3;
+        }
+        total = o;
+    }
+    __syncthreads();
+    for (int64_t e = t; e < B; e += blockDim.x) {
+        const int s = slot_of(e);
+        order[off[s] + atomicAdd(&cur[s], 1)] = (int32_t)e;
+    }
+    if (t < kGroupSlots)
+        for (int p = cnt[t]; p < ((cnt[t] + 3) & ~3); ++p) order[off[t] + p] = -1;
+    for (int i = total + t; i < cap; i += blockDim.x) order[i] = -1;
+}
+
+int launch_group(const int32_t* actions, int64_t B, int n_slots, int32_t* order, int32_t cap, void* stream) {
+    if (n_slots > kGroupSlots || (int64_t)cap < ((B + 3) / 4) * 4 + 3 * (int64_t)n_slots) return -1;
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, (hipStream_t)stream, actions, B, n_slots, order, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace qcart

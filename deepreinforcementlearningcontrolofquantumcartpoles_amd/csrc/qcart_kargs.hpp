@@ -4,6 +4,31 @@
 
 namespace qcart {
 
+// One force slot's factor tables as one contiguous block, every band / level lane-interleaved:
+// row r = l*R + j of band b at element (b*R + j)*64 + l, scan composite e of level v of lane l at
+// (v*kl*kl + e)*64 + l. A wave's j-th read of a band is then one contiguous 64-element run, and the
+// step kernel addresses the block with one buffer descriptor and constant offsets.
+//   lc   complex [kl][R][64]    L[r][r-k]                      (zgbtrs forward)
+//   uc   complex [kl][R][64]    U[r][r+k] / U[r][r]            (zgbtrs backward)
+//   di   complex [R][64]        1 / U[r][r]
+//   m2   real    [10][R][64]    2 Im A[r-d][r] (IHO only; zero unless the reference mirror mode)
+//   tf   complex [7][kl*kl][64] forward Kogge-Stone composites, level 6 = in-row prefix product
+//   tb   complex [7][kl*kl][64] backward composites, level 6 = in-row suffix product
+struct SlotLayout {
+    uint32_t lc, uc, di, m2, tf, tb, bytes;
+};
+constexpr SlotLayout slot_layout(int kl, int R, bool has_m2) {
+    SlotLayout L{};
+    L.lc = 0;
+    L.uc = L.lc + 16u * 64u * (uint32_t)(kl * R);
+    L.di = L.uc + 16u * 64u * (uint32_t)(kl * R);
+    L.m2 = L.di + 16u * 64u * (uint32_t)R;
+    L.tf = L.m2 + (has_m2 ? 8u * 64u * 10u * (uint32_t)R : 0u);
+    L.tb = L.tf + 16u * 64u * 7u * (uint32_t)(kl * kl);
+    L.bytes = L.tb + 16u * 64u * 7u * (uint32_t)(kl * kl);
+    return L;
+}
+
 struct KArgs {
     // state and I/O (device pointers)
     double* psi;               // [B][N] complex interleaved
@@ -29,9 +54,10 @@ struct KArgs {
     int32_t win_lo, win_hi;    // IQO outside-probability window [lo, hi); win_hi <= win_lo: off
     int32_t moment_order;
     int32_t n_obs;
-    int32_t scan_lds;          // step kernel stages Kogge-Stone composites in LDS (Fock families)
-    int32_t lv_f, lv_b;        // max forward / backward scan levels over the slots (LDS image size)
-    uint32_t scan_lds_bytes;   // dynamic LDS per 4-wave block
+    int32_t tab_mode;          // step kernel factor tables: 0 global, 1 LDS (lc/uc/di/m2), 2 + composites
+    uint32_t lds_bytes;        // dynamic LDS per block for tab_mode >= 1
+    const int32_t* order;      // [n_blocks*4] envs grouped by force slot (-1 idle) or null (identity)
+    uint32_t n_blocks;         // step kernel grid
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
     double a2, a3, a4, a5;     // Horner coefficients dt^3/12, dt^4/24, dt^5/80, dt^6/360
@@ -41,13 +67,9 @@ struct KArgs {
     const double* xu;          // Fock X[r][r+1]
     const double* xg;          // grid x_r
     const double* hu;          // IHO H[r][r+2]; HO / grid H[r][r]
-    // per-slot factor tables
-    const double* lc;          // complex [slot][kl][Npad]
-    const double* uc;          // complex [slot][kl][Npad]
-    const double* dinv;        // complex [slot][Npad]
-    const double* m2;          // real    [slot][10][Npad]
-    const double* tf;          // complex [slot][6][64][kl*kl]
-    const double* tb;          // complex [slot][6][64][kl*kl]
+    // per-slot factor blocks (see SlotLayout), slot s at tab + s * slot_bytes
+    const double* tab;
+    uint32_t slot_bytes;
     const int32_t* kf;         // [slot]
     const int32_t* kb;         // [slot]
     const double* force;       // [slot]
@@ -61,5 +83,7 @@ int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mas
                  double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                  void* stream);
 bool have_kernel(int family, int R);
+// envs grouped by force slot into order[cap] (4-aligned groups, -1 padding); qcart_k_group.hip
+int launch_group(const int32_t* actions, int64_t B, int n_slots, int32_t* order, int32_t cap, void* stream);
 
 }  // namespace qcart

@@ -40,6 +40,48 @@ __device__ __forceinline__ cd cmsub(cd acc, cd a, cd b) {  // acc - a*b
     return C(acc.re - (a.re * b.re - a.im * b.im), acc.im - (a.re * b.im + a.im * b.re));
 }
 __device__ __forceinline__ cd ld(const double* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
+// Factor-block reads: one buffer descriptor per slot block (SGPRs), per-lane VGPR offset, constant
+// SGPR / immediate byte offsets. Out-of-range reads return 0 (descriptor bounds = block size).
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double u2d(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+#ifdef QCART_EXPT_NOLOAD   // latency experiment only: results are wrong
+__device__ __forceinline__ cd bld_c(rsrc_t, int voff, int soff) { return C(1e-3 * (double)((voff + soff) & 7), 1e-4); }
+__device__ __forceinline__ double bld_d(rsrc_t, int voff, int soff) { return 1e-6 * (double)((voff + soff) & 7); }
+#else
+__device__ __forceinline__ cd bld_c(rsrc_t r, int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return C(u2d(v[0], v[1]), u2d(v[2], v[3]));
+}
+__device__ __forceinline__ double bld_d(rsrc_t r, int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return u2d(v[0], v[1]);
+}
+#endif
+
+// Diagnostic build only (-DQCART_STAMPS): per-phase cycle shares of the step loop, summed over all
+// waves into qc_stamps[] (read back by qc_debug_stamps). No stamp executes in the shipped build.
+#ifdef QCART_STAMPS
+__device__ unsigned long long qc_stamps[16];
+#define QC_STAMP(ph)                                                                                 \
+    do {                                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+        unsigned long long t_;                                                                       \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+        st_acc[st_ph] += t_ - st_t;                                                                  \
+        st_t = t_;                                                                                   \
+        st_ph = (ph);                                                                                \
+    } while (0)
+#else
+#define QC_STAMP(ph) \
+    do {             \
+    } while (0)
+#endif
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -296,19 +338,127 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
 
 // ---- banded solve (zgbtrs, IHO/simulation_i.cpp:487, QO/simulation_quart.cpp:622) of the
 // precomputed pivot-free LU, in place on b.
-// Composite T_lvl(lane) element e = i*KL + k: from global ([lvl][lane][e]) or, when the wave has
-// staged its own lane's composites in LDS, from the lane-private LDS image ([lvl][e][lane]).
-template <int KL, bool LDS>
-__device__ __forceinline__ cd comp(const double* g, const double* l, int lvl, int e, int lane) {
-    if constexpr (LDS) return ld(l, ((size_t)lvl * KL * KL + e) * 64 + lane);
-    else return ld(g, ((size_t)lvl * 64 + lane) * KL * KL + e);
+// Composite T_lvl(lane) element e = i*KL + k: from global ([lvl][lane][e], lvl < 7) or, when the wave
+// has staged its own lane's composites in LDS, from the lane-private LDS image ([lvl][e][lane]).
+// Factor-table access of one step kernel instance. MODE 0: every read from the slot's global block
+// (buffer loads); MODE 1: lc/uc/di/m2 from the workgroup's shared LDS image of its slot's block;
+// MODE 2: the scan composites too. The LDS image is the block's first SL.tf bytes verbatim,
+// followed by the kept forward levels, the row prefix, the kept backward levels and the row suffix.
+template <int MODE>
+struct Tab {
+    rsrc_t rs;
+    const char* lds;
+    int v16, v8;   // this lane's byte offset in a 16-B / 8-B lane-interleaved run
+    __device__ __forceinline__ cd c(uint32_t off) const {      // lc / uc / di
+        if constexpr (MODE >= 1) {
+            const double2 v = *(const double2*)(lds + off + v16);
+            return C(v.x, v.y);
+        } else {
+            return bld_c(rs, v16, (int)off);
+        }
+    }
+    __device__ __forceinline__ double d(uint32_t off) const {  // m2
+        if constexpr (MODE >= 1) return *(const double*)(lds + off + v8);
+        else return bld_d(rs, v8, (int)off);
+    }
+    __device__ __forceinline__ cd comp(uint32_t off) const {   // scan composites
+        if constexpr (MODE == 2) {
+            const double2 v = *(const double2*)(lds + off + v16);
+            return C(v.x, v.y);
+        } else {
+            return bld_c(rs, v16, (int)off);
+        }
+    }
+};
+
+// DPP with an explicit row mask; rows not in the mask keep 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_dm(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    return mk_d((unsigned)lo, (unsigned)hi);
+}
+// in-row shifts (16-lane DPP rows; sources outside the row read 0)
+template <int D, bool UP>
+__device__ __forceinline__ cd row_shift(cd v) {
+    constexpr int CTRL = UP ? (0x110 + D) : (0x100 + D);   // row_shr:D / row_shl:D
+    return C(dpp_d<CTRL>(v.re), dpp_d<CTRL>(v.im));
 }
 
-template <int KL, int R, bool LDS>
-__device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict__ lc, const double* __restrict__ uc,
-                                           const double* __restrict__ dinv, const double* __restrict__ tf,
-                                           const double* __restrict__ tb, const double* ltf, const double* ltb,
-                                           int kf, int kb, int lane, int base, int Np) {
+// Two-level scan over the wave for the substitution end states s (KL-vector per lane): Kogge-Stone
+// inside each 16-lane row with row_shr/row_shl DPP (nlev <= 4 levels, segmented by the row boundary),
+// then one carry of the neighbouring row's end state (row_bcast:15 upward / wave_shl + row_newbcast:15
+// downward) through the in-row prefix product P. Valid when transfer products over >= 16 lanes are
+// below kScanTol (nlev <= 4); otherwise band_solve runs the full 6-level Kogge-Stone with shuffles.
+template <int KL, bool FWD>
+__device__ __forceinline__ void scan_rows(cd (&s)[KL], const cd (&T)[4][KL * KL], const cd (&P)[KL * KL], int nlev) {
+#pragma unroll
+    for (int lvl = 0; lvl < 4; ++lvl) {
+        if (lvl < nlev) {
+            cd p[KL];
+#pragma unroll
+            for (int k = 0; k < KL; ++k) {
+                if (lvl == 0) p[k] = row_shift<1, FWD>(s[k]);
+                else if (lvl == 1) p[k] = row_shift<2, FWD>(s[k]);
+                else if (lvl == 2) p[k] = row_shift<4, FWD>(s[k]);
+                else p[k] = row_shift<8, FWD>(s[k]);
+            }
+#pragma unroll
+            for (int i = 0; i < KL; ++i)
+#pragma unroll
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], T[lvl][i * KL + k], p[k]);
+        }
+    }
+    cd c[KL];
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+        if constexpr (FWD) {
+            // lane 15 of row r-1 -> every lane of row r (row 0 keeps 0)
+            c[k] = C(dpp_dm<0x142, 0xe>(s[k].re), dpp_dm<0x142, 0xe>(s[k].im));
+        } else {
+            // first lane of row r+1 -> lane 15 of row r (wave_shl:1) -> every lane of row r
+            const cd t = C(shl1(s[k].re), shl1(s[k].im));
+            c[k] = C(dpp_dm<0x15F, 0xf>(t.re), dpp_dm<0x15F, 0xf>(t.im));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < KL; ++i)
+#pragma unroll
+        for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], P[i * KL + k], c[k]);
+}
+
+template <int KL, int MODE>
+__device__ __forceinline__ void load_scan(cd (&T)[4][KL * KL], cd (&P)[KL * KL], const Tab<MODE>& tb, uint32_t lv0,
+                                          uint32_t lvp, int nlev) {
+#pragma unroll
+    for (int lvl = 0; lvl < 4; ++lvl)
+        if (lvl < nlev)
+#pragma unroll
+            for (int e = 0; e < KL * KL; ++e) T[lvl][e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * 1024u);
+#pragma unroll
+    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * 1024u);
+}
+
+#ifdef QCART_STAMPS
+#define QC_SOLVE_STAMP_ARGS , unsigned long long (&st_acc)[16], unsigned long long& st_t, int& st_ph
+#define QC_SOLVE_STAMP_PASS , st_acc, st_t, st_ph
+#else
+#define QC_SOLVE_STAMP_ARGS
+#define QC_SOLVE_STAMP_PASS
+#endif
+// Composite level offsets: forward level l at f0 + l*C, row prefix at fP; backward at b0 + l*C, bP
+// (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
+template <int KL, int R, int MODE, bool M2>
+__device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int kf, int kb,
+                                           int lane QC_SOLVE_STAMP_ARGS) {
+    constexpr SlotLayout SL = slot_layout(KL, R, M2);
+    constexpr uint32_t CB = KL * KL * 1024u;
+    const uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + (uint32_t)kf * CB : SL.tf + 6u * CB;
+    const uint32_t b0 = MODE == 2 ? SL.tf + (uint32_t)(kf + 1) * CB : SL.tb;
+    const uint32_t bP = MODE == 2 ? SL.tf + (uint32_t)(kf + 1 + kb) * CB : SL.tb + 6u * CB;
+    const bool hf = kf <= 4, hb = kb <= 4;
+    cd T[4][KL * KL], P[KL * KL];
     // forward, pass 1 (zero incoming state): lane end state e_l
     cd s[KL];
 #pragma unroll
@@ -317,26 +467,34 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
     for (int j = 0; j < R; ++j) {
         cd y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, ld(lc, (size_t)k * Np + base + j), s[k]);
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
     }
-    // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
-    for (int lvl = 0; lvl < kf; ++lvl) {
-        const int d = 1 << lvl;
-        cd p[KL];
+    QC_STAMP(10);
+    if (hf) {
+        load_scan<KL, MODE>(T, P, tb, f0, fP, kf);
+        scan_rows<KL, true>(s, T, P, kf);
+    } else {
+        // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
+        for (int lvl = 0; lvl < kf; ++lvl) {
+            const int d = 1 << lvl;
+            cd p[KL];
 #pragma unroll
-        for (int k = 0; k < KL; ++k)
-            p[k] = (lvl == 0) ? C(shr1(s[k].re), shr1(s[k].im))
-                              : C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
-        if (lane >= d) {
+            for (int k = 0; k < KL; ++k)
+                p[k] = (lvl == 0) ? C(shr1(s[k].re), shr1(s[k].im))
+                                  : C(__shfl_up(s[k].re, d, 64), __shfl_up(s[k].im, d, 64));
+            if (lane >= d) {
 #pragma unroll
-            for (int i = 0; i < KL; ++i)
+                for (int i = 0; i < KL; ++i)
 #pragma unroll
-                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], comp<KL, LDS>(tf, ltf, lvl, i * KL + k, lane), p[k]);
+                    for (int k = 0; k < KL; ++k)
+                        s[i] = cmac(s[i], tb.comp(f0 + (uint32_t)(lvl * KL * KL + i * KL + k) * 1024u), p[k]);
+            }
         }
     }
+    QC_STAMP(11);
     // incoming state from lane - 1, pass 2
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
@@ -344,45 +502,54 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const double* __restrict_
     for (int j = 0; j < R; ++j) {
         cd y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, ld(lc, (size_t)k * Np + base + j), s[k]);
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
         b[j] = y;
     }
+    QC_STAMP(12);
     // backward, pass 1 (rows high -> low): x_r = dinv_r y_r - sum_k uc_k x_{r+k}
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        cd x = cmul(ld(dinv, base + j), b[j]);
+        cd x = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ld(uc, (size_t)k * Np + base + j), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
     }
-    for (int lvl = 0; lvl < kb; ++lvl) {
-        const int d = 1 << lvl;
-        cd p[KL];
+    QC_STAMP(13);
+    if (hb) {
+        load_scan<KL, MODE>(T, P, tb, b0, bP, kb);
+        scan_rows<KL, false>(s, T, P, kb);
+    } else {
+        for (int lvl = 0; lvl < kb; ++lvl) {
+            const int d = 1 << lvl;
+            cd p[KL];
 #pragma unroll
-        for (int k = 0; k < KL; ++k)
-            p[k] = (lvl == 0) ? C(shl1(s[k].re), shl1(s[k].im))
-                              : C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
-        if (lane + d < 64) {
+            for (int k = 0; k < KL; ++k)
+                p[k] = (lvl == 0) ? C(shl1(s[k].re), shl1(s[k].im))
+                                  : C(__shfl_down(s[k].re, d, 64), __shfl_down(s[k].im, d, 64));
+            if (lane + d < 64) {
 #pragma unroll
-            for (int i = 0; i < KL; ++i)
+                for (int i = 0; i < KL; ++i)
 #pragma unroll
-                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], comp<KL, LDS>(tb, ltb, lvl, i * KL + k, lane), p[k]);
+                    for (int k = 0; k < KL; ++k)
+                        s[i] = cmac(s[i], tb.comp(b0 + (uint32_t)(lvl * KL * KL + i * KL + k) * 1024u), p[k]);
+            }
         }
     }
+    QC_STAMP(14);
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        cd x = cmul(ld(dinv, base + j), b[j]);
+        cd x = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ld(uc, (size_t)k * Np + base + j), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -500,51 +667,51 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
-template <int FAM, int R, bool LDS>
-__global__ __launch_bounds__(256) void k_step(const KArgs a) {
+template <int FAM, int R, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_step(const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
+    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1);
     const int lane = threadIdx.x & 63;
-    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (env >= a.B) return;
-    const int base = lane * R;
-    const int N = a.N, Np = a.Npad;
-    Coef<FAM, R> cf;
-    load_coef<FAM, R>(cf, a, base);
-
-    int slot = a.actions ? a.actions[env] : a.default_action;
+    // env of this wave: a.order (envs grouped by force slot, 4 per block, -1 = idle) or identity
+    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * 4] : (int64_t)blockIdx.x * 4;
+    if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
+    const int64_t env = a.order ? (int64_t)a.order[blockIdx.x * 4 + (threadIdx.x >> 6)]
+                                : (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool active = env >= 0 && env < a.B;
+    // force slot: per wave (MODE 0), per block (MODE >= 1: the host groups envs so that every wave of a
+    // block shares its first env's slot)
+    int slot = a.actions ? a.actions[(MODE >= 1 || !active) ? e0 : env] : a.default_action;
     slot = __builtin_amdgcn_readfirstlane(slot);
     slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
-    const double cF = a.c * a.force[slot];
-    const double* lc = a.lc + (size_t)slot * KL * Np * 2;
-    const double* uc = a.uc + (size_t)slot * KL * Np * 2;
-    const double* dinv = a.dinv + (size_t)slot * Np * 2;
-    const double* m2 = a.m2 + (size_t)slot * 10 * Np;
-    const double* tf = a.tf + (size_t)slot * 6 * 64 * KL * KL * 2;
-    const double* tb = a.tb + (size_t)slot * 6 * 64 * KL * KL * 2;
+    const rsrc_t rs = make_rsrc((const char*)a.tab + (size_t)slot * a.slot_bytes, SL.bytes);
     const int kf = a.kf[slot], kb = a.kb[slot];
-    // Stage this lane's own Kogge-Stone composites into a lane-private LDS image: the scan then
-    // reads them at LDS latency every step without pinning them in registers.
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
-    double* ltf = smem_dyn + (size_t)(threadIdx.x >> 6) * (a.lv_f + a.lv_b) * KL * KL * 64 * 2;
-    double* ltb = ltf + (size_t)a.lv_f * KL * KL * 64 * 2;
-    if constexpr (LDS) {
-        for (int lvl = 0; lvl < kf; ++lvl)
-#pragma unroll
-            for (int e = 0; e < KL * KL; ++e) {
-                const cd v = ld(tf, ((size_t)lvl * 64 + lane) * KL * KL + e);
-                const size_t o = (((size_t)lvl * KL * KL + e) * 64 + lane) * 2;
-                ltf[o] = v.re;
-                ltf[o + 1] = v.im;
+    if constexpr (MODE >= 1) {
+        // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
+        // the 4 waves for all n_steps steps
+        char* img = (char*)smem_dyn;
+        auto copy = [&](uint32_t src, uint32_t dst, uint32_t bytes) {
+            for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 256u * 16u) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, (int)src, 0);
+                *(uint4*)(img + dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
             }
-        for (int lvl = 0; lvl < kb; ++lvl)
-#pragma unroll
-            for (int e = 0; e < KL * KL; ++e) {
-                const cd v = ld(tb, ((size_t)lvl * 64 + lane) * KL * KL + e);
-                const size_t o = (((size_t)lvl * KL * KL + e) * 64 + lane) * 2;
-                ltb[o] = v.re;
-                ltb[o + 1] = v.im;
-            }
+        };
+        copy(0, 0, SL.tf);
+        if constexpr (MODE == 2) {
+            constexpr uint32_t CB = KL * KL * 1024u;
+            copy(SL.tf, SL.tf, (uint32_t)kf * CB);
+            copy(SL.tf + 6u * CB, SL.tf + (uint32_t)kf * CB, CB);
+            copy(SL.tb, SL.tf + (uint32_t)(kf + 1) * CB, (uint32_t)kb * CB);
+            copy(SL.tb + 6u * CB, SL.tf + (uint32_t)(kf + 1 + kb) * CB, CB);
+        }
+        __syncthreads();
     }
+    if (!active) return;
+    const int base = lane * R;
+    const int N = a.N;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+    const double cF = a.c * a.force[slot];
 
     double* gpsi = a.psi + (size_t)env * N * 2;
     cd psi[R];
@@ -578,7 +745,13 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
         n_my = e < 0 ? 0 : (e < n_my ? e : n_my);
     }
     n_my = __builtin_amdgcn_readfirstlane(n_my);
+#ifdef QCART_STAMPS
+    unsigned long long st_acc[16] = {0}, st_t = 0;
+    int st_ph = 9;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");
+#endif
     for (int k = 0; k < n_my; ++k) {
+        QC_STAMP(0);
         if ((k & 63) == 0) {   // lane j: normals of step k + j
             if (a.noise) {
                 const int kk = k + lane;
@@ -597,6 +770,11 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
             if (a.q_out) a.q_out[(size_t)k * a.B + env] = xbar + dW * a.inv_sqrt2g / dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = xbar;
         }
+        // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
+        // reads and their addresses inside the step (LICM would otherwise pin them in registers)
+        int lane_o = lane;
+        asm volatile("" : "+v"(lane_o));
+        const Tab<MODE> tb{rs, (const char*)smem_dyn, lane_o * 16, lane_o * 8};
         const double c1 = 0.5 / sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 / sdt * (dW * dW - dt);
         const double c4 = 0.5 / dt * (dW * dt - dZ), c5 = 0.25 / dt * (dW * dW / 3 - dt) * dW;
         const double c6 = 0.25 * sdt * dW;
@@ -626,6 +804,7 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
                 Yp[j] = C(yr + kY * rel[j].re, yi + kY * rel[j].im);
                 Ym[j] = C(yr - kY * rel[j].re, yi - kY * rel[j].im);
             }
+            QC_STAMP(1);
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)   (IHO:253-264, :551)
             {
                 cd t[R], u[R];
@@ -645,27 +824,44 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = C(acc[j].re + t[j].re, acc[j].im + t[j].im);
             }
+            QC_STAMP(2);
             if constexpr (FAM == 1) {
                 // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  
                 if (a.mirror) {
+                    // the 10 x R band reads are issued in two batches of 5 bands, each fenced from the
+                    // arithmetic (sched_barrier) so they are in flight together: one exposed latency per
+                    // batch instead of one per read
+                    double sre[R], sim[R];
+#pragma unroll
+                    for (int j = 0; j < R; ++j) sre[j] = sim[j] = 0.0;
                     cd lo[10];
-                    make_lo<R, 10>(D1, lo, lane);
 #pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        double sre = 0.0, sim = 0.0;
+                    for (int h = 0; h < 2; ++h) {
+                        double mv[5][R];
 #pragma unroll
-                        for (int d = 1; d <= 10; ++d) {
-                            const double mv = m2[(size_t)(d - 1) * Np + base + j];
-                            const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
-                                                       : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
-                            sre += mv * dv.re;
-                            sim += mv * dv.im;
-                        }
-                        acc[j] = C(acc[j].re + sim, acc[j].im - sre);
+                        for (int dd = 0; dd < 5; ++dd)
+#pragma unroll
+                            for (int j = 0; j < R; ++j)
+                                mv[dd][j] = tb.d(SL.m2 + (uint32_t)((5 * h + dd) * R + j) * 512u);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (h == 0) make_lo<R, 10>(D1, lo, lane);
+#pragma unroll
+                        for (int j = 0; j < R; ++j)
+#pragma unroll
+                            for (int dd = 0; dd < 5; ++dd) {
+                                const int d = 5 * h + dd + 1;
+                                const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
+                                                           : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
+                                sre[j] += mv[dd][j] * dv.re;
+                                sim[j] += mv[dd][j] * dv.im;
+                            }
                     }
+#pragma unroll
+                    for (int j = 0; j < R; ++j) acc[j] = C(acc[j].re + sim[j], acc[j].im - sre[j]);
                 }
             }
         }
+        QC_STAMP(3);
         // Y+- (D1ImRe IHO:301-318 + D2 precomputed), unnormalised means
         double yp, ym;
         {
@@ -682,6 +878,7 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
             yp = a.w * s[0];
             ym = a.w * s[1];
             const double kIm = c1 - c6;
+            QC_STAMP(4);
             // + branch
             {
                 cd hY[R], xx[R];
@@ -705,6 +902,7 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
                     xYp[j] = pm;
                 }
             }
+            QC_STAMP(5);
             // - branch
             {
                 cd hY[R], xx[R];
@@ -724,6 +922,7 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
                     acc[j] = C(acc[j].re + kRe * qre + kD * xYm[j].re, acc[j].im + kRe * qim + kD * xYm[j].im);
                 }
             }
+            QC_STAMP(6);
             // Phi+- : D2 with fresh unnormalised means (IHO:321-332, :480)
             {
                 cd xPp[R], xPm[R];
@@ -744,8 +943,10 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
                 }
             }
         }
+        QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R, LDS>(acc, lc, uc, dinv, tf, tb, ltf, ltb, kf, kb, lane, base, Np);
+        band_solve<KL, R, MODE, FAM == 1>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);
+        QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
             cd xn[R];
@@ -776,6 +977,11 @@ __global__ __launch_bounds__(256) void k_step(const KArgs a) {
             if (win_on && term < 0 && 1.0 - a.h * (s[4] * scale) * scale > 0.5) term = k + 1;
         }
     }
+#ifdef QCART_STAMPS
+    QC_STAMP(9);
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) atomicAdd(&qc_stamps[i], st_acc[i]);
+#endif
     // write back
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -962,6 +1168,22 @@ namespace qcart {
 
 static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
+template <int FAM, int R, int MODE>
+int launch_step_mode(const KArgs& a, hipStream_t st) {
+    const dim3 grid(a.n_blocks), block(256);
+    if (MODE >= 1) {
+        static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+        if (!attr_set) {
+            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024) != hipSuccess)
+                return -3;
+            attr_set = true;
+        }
+    }
+    hipLaunchKernelGGL((k_step<FAM, R, MODE>), grid, block, MODE >= 1 ? a.lds_bytes : 0, st, a);
+    return 0;
+}
+
 // per-family launch entry points, instantiated in qcart_k_{ho,iho,grid}.hip
 template <int FAM, int R>
 int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
@@ -970,18 +1192,10 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
     if (kind == 0) {
-        if (FAM <= 1 && a.scan_lds) {
-            static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
-            if (!attr_set) {
-                if (hipFuncSetAttribute((const void*)k_step<FAM, R, (FAM <= 1)>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-                    return -3;
-                attr_set = true;
-            }
-            hipLaunchKernelGGL((k_step<FAM, R, (FAM <= 1)>), grid, block, a.scan_lds_bytes, st, a);
-        }
-        else
-            hipLaunchKernelGGL((k_step<FAM, R, false>), grid, block, 0, st, a);
+        const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2>(a, st)
+                     : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1>(a, st)
+                                       : launch_step_mode<FAM, R, 0>(a, st);
+        if (rc) return rc;
     }
     else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R>), grid, block, 0, st, a);
     else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R>), grid, block, 0, st, a, what, xth, out);

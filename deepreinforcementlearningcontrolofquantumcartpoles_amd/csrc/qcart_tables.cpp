@@ -232,8 +232,19 @@ int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost
         Qk[l] = Q;
     }
     const size_t blk = (size_t)kl * kl;
-    act.tf.assign((size_t)kMaxLevels * kWave * blk, cplx(0, 0));
-    act.tb.assign((size_t)kMaxLevels * kWave * blk, cplx(0, 0));
+    act.tf.assign((size_t)kTabLevels * kWave * blk, cplx(0, 0));
+    act.tb.assign((size_t)kTabLevels * kWave * blk, cplx(0, 0));
+    // in-row (16-lane DPP row) products for the two-level scan: forward Pf(l) = Phi_l .. Phi_{row start},
+    // backward Pb(l) = Psi_l .. Psi_{row end}; they carry a neighbouring row's end state into the row
+    {
+        std::vector<Mat> Pf(kWave), Pb(kWave);
+        for (int l = 0; l < kWave; l++) Pf[l] = (l % 16 == 0) ? Tk[l] : matmul(Tk[l], Pf[l - 1], kl);
+        for (int l = kWave - 1; l >= 0; l--) Pb[l] = (l % 16 == 15) ? Qk[l] : matmul(Qk[l], Pb[l + 1], kl);
+        for (int l = 0; l < kWave; l++) {
+            std::copy(Pf[l].begin(), Pf[l].end(), act.tf.begin() + ((size_t)kRowPrefix * kWave + l) * blk);
+            std::copy(Pb[l].begin(), Pb[l].end(), act.tb.begin() + ((size_t)kRowPrefix * kWave + l) * blk);
+        }
+    }
     for (int lvl = 0; lvl < kMaxLevels; lvl++) {
         const int d = 1 << lvl;
         double mf = 0, mb = 0;

@@ -24,6 +24,8 @@ using cplx = std::complex<double>;
 
 constexpr int kWave = 64;
 constexpr int kMaxLevels = 6;     // log2(64)
+constexpr int kTabLevels = 7;     // per direction: 6 Kogge-Stone levels + the in-row prefix product
+constexpr int kRowPrefix = 6;     // table level holding the in-row prefix product (16-lane rows)
 constexpr int kMirrorBands = 10;  // offsets -1..-10 of tril(Im A, -1) for the IHO (5*kl)
 constexpr double kScanTol = 1e-22;  // drop Kogge-Stone levels whose composites are below this
 
@@ -49,8 +51,8 @@ struct ActHost {
     std::vector<cplx> uc;             // [kl][Npad]  U[r][r+k] / U[r][r]
     std::vector<cplx> dinv;           // [Npad]      1 / U[r][r]
     std::vector<double> m2;           // [10][Npad]  2 Im A[r][r-d]   (IHO reference mode only)
-    std::vector<cplx> tf;             // [6][64][kl*kl] forward composites  T_k(l)
-    std::vector<cplx> tb;             // [6][64][kl*kl] backward composites Q_k(l)
+    std::vector<cplx> tf;             // [7][64][kl*kl] forward composites  T_k(l); [6]: row prefix
+    std::vector<cplx> tb;             // [7][64][kl*kl] backward composites Q_k(l); [6]: row suffix
     double max_tf[kMaxLevels] = {0}, max_tb[kMaxLevels] = {0};
 };
 

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Per-phase cycle shares of the IHO step loop from the diagnostic stamps build
+(make expt EXPT=-DQCART_STAMPS NAME=stamps; run with QCART_LIB=<pkg>/libqcart_stamps.so).
+Read the SHARES, not the absolute time (the stamps fence the schedule)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper  # noqa: E402
+
+PHASES = ["noise+D1", "term7", "mirror", "Y means", "+branch", "-branch", "Phi", "solve:fwd1", "normalise", "tail",
+          "solve:fscan", "solve:fwd2", "solve:bwd1", "solve:bscan", "solve:bwd2", "-"]
+
+
+def main():
+    n_max = int(sys.argv[1]) if len(sys.argv) > 1 else 511
+    a_mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    B = 16384
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max, a_mode=a_mode)
+    st = Stepper(ph, B, 0, seed=1)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=16)
+    acts = torch.randint(0, 21, (B,), device="cuda", dtype=torch.int32)
+    L = _lib.lib()
+    f = L.qc_debug_stamps
+    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    buf = (ctypes.c_ulonglong * 16)()
+    st.step(psi, acts, 80)
+    torch.cuda.synchronize()
+    f(buf)
+    st.step(psi, acts, 80)
+    torch.cuda.synchronize()
+    f(buf)
+    tot = sum(buf)
+    print(f"IHO N={ph.dim} a_mode={a_mode}: total {tot / (B * 80):.0f} cycles per wave-step (stamped build)")
+    for name, v in zip(PHASES, buf):
+        print(f"  {name:10s} {v / (B * 80):8.0f} cyc  {100 * v / tot:5.1f} %")
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,7 @@ struct qc_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     int R = 0;
+    int wpb = 4;   // envs per step workgroup (step_waves)
     bool mirror = false;
     OpHost op;
     std::vector<ActHost> acts;
@@ -203,7 +204,7 @@ KArgs base_args(const qc_handle* h) {
         a.lds_bytes = (uint32_t)(mode == 2 ? t2 : (mode == 1 ? t1 : 0));
     }
     a.order = nullptr;
-    a.n_blocks = (uint32_t)((p.batch + 3) / 4);
+    a.n_blocks = (uint32_t)((p.batch + h->wpb - 1) / h->wpb);
     a.n_obs = qc_n_obs(h);
     a.dt = p.dt;
     a.sqrt_dt = std::sqrt(p.dt);
@@ -287,6 +288,12 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     h->R = pick_R(p->family, probe.N);
     if (h->R < 0 || !have_kernel(p->family, h->R)) {
         set_create_err("no kernel instantiated for N = " + std::to_string(probe.N));
+        delete h;
+        return QC_ENOTBUILT;
+    }
+    h->wpb = step_waves(p->family, h->R);
+    if (h->wpb <= 0) {
+        set_create_err("no step kernel for N = " + std::to_string(probe.N));
         delete h;
         return QC_ENOTBUILT;
     }
@@ -419,7 +426,8 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     if (actions) {
         // group envs by force slot, padded to whole 4-env blocks: every block then shares one slot's
         // tables (the per-block LDS image); order within a slot does not change any result
-        const size_t cap = (size_t)((h->p.batch + 3) / 4) * 4 + 4 * (size_t)kMaxSlots;
+        const size_t W = (size_t)h->wpb;
+        const size_t cap = (size_t)((h->p.batch + W - 1) / W) * W + W * (size_t)kMaxSlots;
         if (h->order_cap < cap) {
             if (h->d_order) (void)hipFree(h->d_order);
             h->d_order = nullptr;
@@ -428,10 +436,10 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
             h->order_cap = cap;
         }
-        if (launch_group(actions, h->p.batch, (int)h->acts.size(), h->d_order, (int32_t)cap, h->stream))
+        if (launch_group(actions, h->p.batch, (int)h->acts.size(), (int)W, h->d_order, (int32_t)cap, h->stream))
             return fail(h, QC_EHIP, "group kernel launch failed");
         a.order = h->d_order;
-        a.n_blocks = (uint32_t)(cap / 4);
+        a.n_blocks = (uint32_t)(cap / W);
     }
     int rc = launch_step(h->p.family, h->R, a, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");

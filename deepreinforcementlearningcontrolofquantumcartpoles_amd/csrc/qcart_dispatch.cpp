@@ -35,6 +35,12 @@ bool have_kernel(int family, int R) {
     return false;
 }
 
+int step_waves(int family, int R) {
+    KArgs a{};
+    a.B = 1;
+    return route(family, R, 4, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr);
+}
+
 int launch_step(int family, int R, const KArgs& a, void* stream) {
     return route(family, R, 0, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, stream);
 }

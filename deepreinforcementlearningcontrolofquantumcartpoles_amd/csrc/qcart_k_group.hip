@@ -1,4 +1,4 @@
-// qcart_k_group.hip — groups the envs of a step call by force slot so that each 4-wave workgroup of
+// qcart_k_group.hip — groups the envs of a step call by force slot so that each workgroup of
 // the step kernel shares one slot's factor tables through LDS. One workgroup: LDS histogram of the
 // slots, 4-aligned group offsets, then a scatter of env ids (order inside a group is arbitrary and
 // does not affect any result: envs are independent). Unused entries are -1 (idle waves).
@@ -11,7 +11,7 @@ namespace qcart {
 
 constexpr int kGroupSlots = 64;
 
-__global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ actions, int64_t B, int n_slots,
+__global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ actions, int64_t B, int n_slots, int g,
                                                 int32_t* __restrict__ order, int32_t cap) {
     __shared__ int cnt[kGroupSlots], off[kGroupSlots], cur[kGroupSlots];
     __shared__ int total;
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
         int o = 0;
         for (int s = 0; s < kGroupSlots; ++s) {
             off[s] = o;
-            o += (cnt[s] + 3) & ~3;
+            o += (cnt[s] + g - 1) / g * g;
         }
         total = o;
     }
@@ -41,13 +41,15 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
         order[off[s] + atomicAdd(&cur[s], 1)] = (int32_t)e;
     }
     if (t < kGroupSlots)
-        for (int p = cnt[t]; p < ((cnt[t] + 3) & ~3); ++p) order[off[t] + p] = -1;
+        for (int p = cnt[t]; p < (cnt[t] + g - 1) / g * g; ++p) order[off[t] + p] = -1;
     for (int i = total + t; i < cap; i += blockDim.x) order[i] = -1;
 }
 
-int launch_group(const int32_t* actions, int64_t B, int n_slots, int32_t* order, int32_t cap, void* stream) {
-    if (n_slots > kGroupSlots || (int64_t)cap < ((B + 3) / 4) * 4 + 3 * (int64_t)n_slots) return -1;
-    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, (hipStream_t)stream, actions, B, n_slots, order, cap);
+int launch_group(const int32_t* actions, int64_t B, int n_slots, int gran, int32_t* order, int32_t cap,
+                 void* stream) {
+    if (n_slots > kGroupSlots || gran < 1 || (int64_t)cap < (B + gran - 1) / gran * gran + (int64_t)(gran - 1) * n_slots)
+        return -1;
+    hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, (hipStream_t)stream, actions, B, n_slots, gran, order, cap);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -56,7 +56,7 @@ struct KArgs {
     int32_t n_obs;
     int32_t tab_mode;          // step kernel factor tables: 0 global, 1 LDS (lc/uc/di/m2), 2 + composites
     uint32_t lds_bytes;        // dynamic LDS per block for tab_mode >= 1
-    const int32_t* order;      // [n_blocks*4] envs grouped by force slot (-1 idle) or null (identity)
+    const int32_t* order;      // [n_blocks*W] envs grouped by force slot (-1 idle) or null (identity)
     uint32_t n_blocks;         // step kernel grid
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
@@ -83,7 +83,9 @@ int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mas
                  double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                  void* stream);
 bool have_kernel(int family, int R);
-// envs grouped by force slot into order[cap] (4-aligned groups, -1 padding); qcart_k_group.hip
-int launch_group(const int32_t* actions, int64_t B, int n_slots, int32_t* order, int32_t cap, void* stream);
+int step_waves(int family, int R);   // envs (waves) per step-kernel workgroup
+// envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
+int launch_group(const int32_t* actions, int64_t B, int n_slots, int gran, int32_t* order, int32_t cap,
+                 void* stream);
 
 }  // namespace qcart

@@ -258,6 +258,36 @@ __device__ __forceinline__ void apply_x(const cd (&v)[R], cd (&o)[R], const Coef
     }
 }
 
+// H v (the force-free Hamiltonian; IHO/simulation_i.cpp:75-99, HO/simulation.cpp:69-80, QO/simulation_quart.cpp:
+// 40-58)
+template <int FAM, int R>
+__device__ __forceinline__ void apply_h(const cd (&v)[R], cd (&oh)[R], const Coef<FAM, R>& cf, int lane) {
+    if constexpr (FAM == 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) oh[j] = C(cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
+    } else if constexpr (FAM == 1) {
+        cd e[R + 4];
+        make_ext<R, 2>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            oh[j] = C(cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re, cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
+    } else {
+        cd e[R + 8];
+        make_ext<R, 4>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+#pragma unroll
+            for (int d = 1; d <= 4; ++d) {
+                re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
+                im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
+            }
+            const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
+            oh[j] = C(in ? re : 0.0, in ? im : 0.0);
+        }
+    }
+}
+
 // H v and X v with one halo exchange
 template <int FAM, int R>
 __device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)[R], const Coef<FAM, R>& cf,
@@ -298,10 +328,33 @@ __device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)
 template <int FAM, int R>
 __device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF, const Coef<FAM, R>& cf,
                                          int lane) {
-    cd hx[R], xx[R];
-    apply_hx<FAM, R>(v, hx, xx, cf, lane);
+    // fused per row (no full-length H v / X v temporaries: keeps the step within 256 VGPRs)
+    if constexpr (FAM == 1) {
+        cd e[R + 4];
+        make_ext<R, 2>(v, e, lane);
 #pragma unroll
-    for (int j = 0; j < R; ++j) u[j] = C(hx[j].re - cF * xx[j].re, hx[j].im - cF * xx[j].im);
+        for (int j = 0; j < R; ++j) {
+            const double hre = cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re;
+            const double him = cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im;
+            const double xre = cf.xu[j + 1] * e[j + 3].re + cf.xu[j] * e[j + 1].re;
+            const double xim = cf.xu[j + 1] * e[j + 3].im + cf.xu[j] * e[j + 1].im;
+            u[j] = C(hre - cF * xre, him - cF * xim);
+        }
+    } else if constexpr (FAM == 0) {
+        cd e[R + 2];
+        make_ext<R, 1>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double xre = cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re;
+            const double xim = cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im;
+            u[j] = C(cf.hu[j] * v[j].re - cF * xre, cf.hu[j] * v[j].im - cF * xim);
+        }
+    } else {
+        cd hx[R], xx[R];
+        apply_hx<FAM, R>(v, hx, xx, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) u[j] = C(hx[j].re - cF * xx[j].re, hx[j].im - cF * xx[j].im);
+    }
 }
 
 // ---- counter-based noise (oracle: qo_normals)
@@ -667,16 +720,25 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
+// waves (envs) per step workgroup: 8 (two per SIMD) where the step fits 256 VGPRs, else 4
+#ifndef QCART_W8_MAX_R
+#define QCART_W8_MAX_R 8
+#endif
+template <int FAM, int R>
+constexpr int kStepWaves = (FAM <= 1 && R <= QCART_W8_MAX_R) ? 8 : 4;
+
 template <int FAM, int R, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_step(const KArgs a) {
+__global__ __launch_bounds__((64 * kStepWaves<FAM, R>))
+__attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R> / 4)))) void k_step(const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
+    constexpr int W = kStepWaves<FAM, R>;
     constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1);
     const int lane = threadIdx.x & 63;
-    // env of this wave: a.order (envs grouped by force slot, 4 per block, -1 = idle) or identity
-    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * 4] : (int64_t)blockIdx.x * 4;
+    // env of this wave: a.order (envs grouped by force slot, W per block, -1 = idle) or identity
+    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * W] : (int64_t)blockIdx.x * W;
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
-    const int64_t env = a.order ? (int64_t)a.order[blockIdx.x * 4 + (threadIdx.x >> 6)]
-                                : (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t env = a.order ? (int64_t)a.order[blockIdx.x * W + (threadIdx.x >> 6)]
+                                : (int64_t)blockIdx.x * W + (threadIdx.x >> 6);
     const bool active = env >= 0 && env < a.B;
     // force slot: per wave (MODE 0), per block (MODE >= 1: the host groups envs so that every wave of a
     // block shares its first env's slot)
@@ -691,7 +753,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // the 4 waves for all n_steps steps
         char* img = (char*)smem_dyn;
         auto copy = [&](uint32_t src, uint32_t dst, uint32_t bytes) {
-            for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 256u * 16u) {
+            for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 64u * W * 16u) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, (int)src, 0);
                 *(uint4*)(img + dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
             }
@@ -736,6 +798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
+    const double inv_sdt = 1.0 / sdt, inv_dt = 1.0 / dt;
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
@@ -765,9 +828,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
         // go_one_step: IHO/simulation_i.cpp:432-489
-        const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 / 1.7320508075688772);
+        const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
         if (lane == 0) {
-            if (a.q_out) a.q_out[(size_t)k * a.B + env] = xbar + dW * a.inv_sqrt2g / dt;
+            if (a.q_out) a.q_out[(size_t)k * a.B + env] = xbar + dW * a.inv_sqrt2g * inv_dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = xbar;
         }
         // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
@@ -775,173 +838,159 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         int lane_o = lane;
         asm volatile("" : "+v"(lane_o));
         const Tab<MODE> tb{rs, (const char*)smem_dyn, lane_o * 16, lane_o * 8};
-        const double c1 = 0.5 / sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 / sdt * (dW * dW - dt);
-        const double c4 = 0.5 / dt * (dW * dt - dZ), c5 = 0.25 / dt * (dW * dW / 3 - dt) * dW;
+        const double c1 = 0.5 * inv_sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 * inv_sdt * (dW * dW - dt);
+        const double c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
         const double c6 = 0.25 * sdt * dW;
 
-        cd acc[R], Yp[R], Ym[R];
+        // Live vectors are kept to at most five R-row complex vectors (plus one halo) at any point so
+        // the whole step fits 256 VGPRs: two waves per SIMD. Phases (go_one_step, IHO:432-489):
+        //   A  rel = (X - xbar) psi, D1 = -i H_F psi - g/4 (X - xbar) rel          (D1: IHO:279-298)
+        //   B  u = A D1 (term7, Horner in H_F: IHO:253-264, :551)
+        //   C  acc = psi + kA rel + k2 D1 + u + mirror(D1);  psi <- Y0 = psi + dt D1
+        //   D  Y- branch, then Y+ branch (D1ImRe IHO:301-318, D2 IHO:320-333)
+        //   E  Phi+- means from <Y+, X rel+> products (no X Phi+- applications)
+        cd acc[R], rel[R], D1[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
+        apply_h<FAM, R>(psi, D1, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)   // D1 = -i (H psi - cF X psi)
+            D1[j] = C(D1[j].im - cF * xp[j].im, -(D1[j].re - cF * xp[j].re));
         {
-            // D1 (IHO:279-298), D2 (IHO:320-333)
-            cd rel[R], D1[R];
+            cd xr[R];
+            apply_x<FAM, R>(rel, xr, cf, lane);
 #pragma unroll
-            for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
-            {
-                cd hp[R], xr[R], tmp[R];
-                apply_hx<FAM, R>(psi, hp, tmp, cf, lane);
-                apply_x<FAM, R>(rel, xr, cf, lane);
+            for (int j = 0; j < R; ++j)
+                D1[j] = C(D1[j].re - g4 * (xr[j].re - xbar * rel[j].re), D1[j].im - g4 * (xr[j].im - xbar * rel[j].im));
+        }
+        QC_STAMP(1);
+        {
+            // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)
+            cd t[R];
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double hre = hp[j].re - cF * xp[j].re, him = hp[j].im - cF * xp[j].im;
-                    const double qre = xr[j].re - xbar * rel[j].re, qim = xr[j].im - xbar * rel[j].im;
-                    D1[j] = C(him - g4 * qre, -hre - g4 * qim);
-                }
-            }
-            const double kA = (dW - 2.0 * c4) * beta, kY = sdt * beta, k2 = 2.0 * c2;
+            for (int j = 0; j < R; ++j) t[j] = C(-a.a5 * D1[j].im, a.a5 * D1[j].re);
+            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re - a.a4 * D1[j].re, acc[j].im - a.a4 * D1[j].im);
+            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a3 * D1[j].im, acc[j].im - a.a3 * D1[j].re);
+            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a2 * D1[j].re, acc[j].im + a.a2 * D1[j].im);
+            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+            apply_hf<FAM, R>(acc, t, cF, cf, lane);
+            const double kA = (dW - 2.0 * c4) * beta, k2 = 2.0 * c2;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re, psi[j].im + kA * rel[j].im + k2 * D1[j].im);
-                const double yr = psi[j].re + dt * D1[j].re, yi = psi[j].im + dt * D1[j].im;
-                Yp[j] = C(yr + kY * rel[j].re, yi + kY * rel[j].im);
-                Ym[j] = C(yr - kY * rel[j].re, yi - kY * rel[j].im);
+                acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re + t[j].re,
+                           psi[j].im + kA * rel[j].im + k2 * D1[j].im + t[j].im);
+                psi[j] = C(psi[j].re + dt * D1[j].re, psi[j].im + dt * D1[j].im);   // Y0
             }
-            QC_STAMP(1);
-            // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)   (IHO:253-264, :551)
-            {
-                cd t[R], u[R];
+        }
+        QC_STAMP(2);
+        if constexpr (FAM == 1) {
+            // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  (SURVEY App. C H1); the band
+            // reads go in batches of MB bands fenced from the arithmetic so each batch is in flight at once
+            if (a.mirror) {
+                constexpr int MB = 1;
+                cd lo[10];
+                make_lo<R, 10>(D1, lo, lane);
 #pragma unroll
-                for (int j = 0; j < R; ++j) t[j] = C(-a.a5 * D1[j].im, a.a5 * D1[j].re);
-                apply_hf<FAM, R>(t, u, cF, cf, lane);
+                for (int h = 0; h < 10 / MB; ++h) {
+                    double mv[MB][R];
 #pragma unroll
-                for (int j = 0; j < R; ++j) t[j] = C(u[j].re - a.a4 * D1[j].re, u[j].im - a.a4 * D1[j].im);
-                apply_hf<FAM, R>(t, u, cF, cf, lane);
+                    for (int dd = 0; dd < MB; ++dd)
 #pragma unroll
-                for (int j = 0; j < R; ++j) t[j] = C(u[j].re + a.a3 * D1[j].im, u[j].im - a.a3 * D1[j].re);
-                apply_hf<FAM, R>(t, u, cF, cf, lane);
+                        for (int j = 0; j < R; ++j) mv[dd][j] = tb.d(SL.m2 + (uint32_t)((MB * h + dd) * R + j) * 512u);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = 0; j < R; ++j) t[j] = C(u[j].re + a.a2 * D1[j].re, u[j].im + a.a2 * D1[j].im);
-                apply_hf<FAM, R>(t, u, cF, cf, lane);
-                apply_hf<FAM, R>(u, t, cF, cf, lane);
+                    for (int j = 0; j < R; ++j)
 #pragma unroll
-                for (int j = 0; j < R; ++j) acc[j] = C(acc[j].re + t[j].re, acc[j].im + t[j].im);
-            }
-            QC_STAMP(2);
-            if constexpr (FAM == 1) {
-                // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  
-                if (a.mirror) {
-                    // the 10 x R band reads are issued in two batches of 5 bands, each fenced from the
-                    // arithmetic (sched_barrier) so they are in flight together: one exposed latency per
-                    // batch instead of one per read
-                    double sre[R], sim[R];
-#pragma unroll
-                    for (int j = 0; j < R; ++j) sre[j] = sim[j] = 0.0;
-                    cd lo[10];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        double mv[5][R];
-#pragma unroll
-                        for (int dd = 0; dd < 5; ++dd)
-#pragma unroll
-                            for (int j = 0; j < R; ++j)
-                                mv[dd][j] = tb.d(SL.m2 + (uint32_t)((5 * h + dd) * R + j) * 512u);
-                        __builtin_amdgcn_sched_barrier(0);
-                        if (h == 0) make_lo<R, 10>(D1, lo, lane);
-#pragma unroll
-                        for (int j = 0; j < R; ++j)
-#pragma unroll
-                            for (int dd = 0; dd < 5; ++dd) {
-                                const int d = 5 * h + dd + 1;
-                                const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
-                                                           : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
-                                sre[j] += mv[dd][j] * dv.re;
-                                sim[j] += mv[dd][j] * dv.im;
-                            }
-                    }
-#pragma unroll
-                    for (int j = 0; j < R; ++j) acc[j] = C(acc[j].re + sim[j], acc[j].im - sre[j]);
+                        for (int dd = 0; dd < MB; ++dd) {
+                            const int d = MB * h + dd + 1;
+                            const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
+                                                       : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
+                            acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
+                        }
                 }
             }
         }
         QC_STAMP(3);
-        // Y+- (D1ImRe IHO:301-318 + D2 precomputed), unnormalised means
-        double yp, ym;
+        const double kY = sdt * beta, kIm = c1 - c6, kP = sdt * beta;
         {
-            cd xYp[R], xYm[R];
-            apply_x<FAM, R>(Yp, xYp, cf, lane);
-            apply_x<FAM, R>(Ym, xYm, cf, lane);
-            double s[2] = {0.0, 0.0};
+            // Y- branch: Y- = Y0 - kY rel; Y+ kept in psi's registers
+            cd Ym[R], xY[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                s[0] += Yp[j].re * xYp[j].re + Yp[j].im * xYp[j].im;
-                s[1] += Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im;
+                Ym[j] = C(psi[j].re - kY * rel[j].re, psi[j].im - kY * rel[j].im);
+                psi[j] = C(psi[j].re + kY * rel[j].re, psi[j].im + kY * rel[j].im);   // Y+
             }
-            wave_sum<2>(s);
-            yp = a.w * s[0];
-            ym = a.w * s[1];
-            const double kIm = c1 - c6;
-            QC_STAMP(4);
-            // + branch
+            apply_x<FAM, R>(Ym, xY, cf, lane);
+            double sm[1] = {0.0};
+#pragma unroll
+            for (int j = 0; j < R; ++j) sm[0] += Ym[j].re * xY[j].re + Ym[j].im * xY[j].im;
+            wave_sum<1>(sm);
+            const double ym = a.w * sm[0];
             {
-                cd hY[R], xx[R];
-                apply_hx<FAM, R>(Yp, hY, xx, cf, lane);
+                cd hY[R];
+                apply_h<FAM, R>(Ym, hY, cf, lane);
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const double hre = hY[j].re - cF * xYp[j].re, him = hY[j].im - cF * xYp[j].im;
-                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) * (-i H_F Y+)
-                    xYp[j] = C(xYp[j].re - yp * Yp[j].re, xYp[j].im - yp * Yp[j].im);   // rel+
-                }
-                cd xr[R];
-                apply_x<FAM, R>(xYp, xr, cf, lane);
-                const double kRe = -(c1 + c2) * g4, kD = (c3 + c4 - c5) * beta, kP = sdt * beta;
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double qre = xr[j].re - yp * xYp[j].re, qim = xr[j].im - yp * xYp[j].im;
-                    acc[j] = C(acc[j].re + kRe * qre + kD * xYp[j].re, acc[j].im + kRe * qim + kD * xYp[j].im);
-                    const cd pp = C(Yp[j].re + kP * xYp[j].re, Yp[j].im + kP * xYp[j].im);    // Phi+
-                    const cd pm = C(Yp[j].re - kP * xYp[j].re, Yp[j].im - kP * xYp[j].im);    // Phi-
-                    Yp[j] = pp;
-                    xYp[j] = pm;
+                    const double hre = hY[j].re - cF * xY[j].re, him = hY[j].im - cF * xY[j].im;
+                    acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);   // -(c1-c6) (-i H_F Y-)
+                    xY[j] = C(xY[j].re - ym * Ym[j].re, xY[j].im - ym * Ym[j].im);   // rel-
                 }
             }
+            apply_x<FAM, R>(xY, Ym, cf, lane);   // X rel- (Y- no longer needed)
+            const double kRe = -(c2 - c1) * g4, kD = (c4 - c3 + c5) * beta;
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                acc[j] = C(acc[j].re + kRe * (Ym[j].re - ym * xY[j].re) + kD * xY[j].re,
+                           acc[j].im + kRe * (Ym[j].im - ym * xY[j].im) + kD * xY[j].im);
+        }
+        QC_STAMP(4);
+        {
+            // Y+ branch (Y+ in psi); keeps X Y+, rel+ and X rel+ for the Phi means
+            cd xY[R], rp[R], xrp[R];
+            apply_x<FAM, R>(psi, xY, cf, lane);
+            double sp[1] = {0.0};
+#pragma unroll
+            for (int j = 0; j < R; ++j) sp[0] += psi[j].re * xY[j].re + psi[j].im * xY[j].im;
+            wave_sum<1>(sp);
+            const double yp = a.w * sp[0];
+            {
+                cd hY[R];
+                apply_h<FAM, R>(psi, hY, cf, lane);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double hre = hY[j].re - cF * xY[j].re, him = hY[j].im - cF * xY[j].im;
+                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) (-i H_F Y+)
+                    rp[j] = C(xY[j].re - yp * psi[j].re, xY[j].im - yp * psi[j].im);   // rel+
+                }
+            }
+            apply_x<FAM, R>(rp, xrp, cf, lane);
+            const double kRe = -(c1 + c2) * g4, kD = (c3 + c4 - c5) * beta;
             QC_STAMP(5);
-            // - branch
-            {
-                cd hY[R], xx[R];
-                apply_hx<FAM, R>(Ym, hY, xx, cf, lane);
+            // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
+            //   pp/pm = yp +- w kP (<Y+, X rel+> + <rel+, X Y+>) + w kP^2 <rel+, X rel+>
+            double d2[2] = {0.0, 0.0};
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double hre = hY[j].re - cF * xYm[j].re, him = hY[j].im - cF * xYm[j].im;
-                    acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);   // -(c1-c6) * (-i H_F Y-)
-                    xYm[j] = C(xYm[j].re - ym * Ym[j].re, xYm[j].im - ym * Ym[j].im);   // rel-
-                }
-                cd xr[R];
-                apply_x<FAM, R>(xYm, xr, cf, lane);
-                const double kRe = -(c2 - c1) * g4, kD = (c4 - c3 + c5) * beta;
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double qre = xr[j].re - ym * xYm[j].re, qim = xr[j].im - ym * xYm[j].im;
-                    acc[j] = C(acc[j].re + kRe * qre + kD * xYm[j].re, acc[j].im + kRe * qim + kD * xYm[j].im);
-                }
+            for (int j = 0; j < R; ++j) {
+                acc[j] = C(acc[j].re + kRe * (xrp[j].re - yp * rp[j].re) + kD * rp[j].re,
+                           acc[j].im + kRe * (xrp[j].im - yp * rp[j].im) + kD * rp[j].im);
+                d2[0] += psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xY[j].re + rp[j].im * xY[j].im;
+                d2[1] += rp[j].re * xrp[j].re + rp[j].im * xrp[j].im;
             }
+            wave_sum<2>(d2);
             QC_STAMP(6);
-            // Phi+- : D2 with fresh unnormalised means (IHO:321-332, :480)
-            {
-                cd xPp[R], xPm[R];
-                apply_x<FAM, R>(Yp, xPp, cf, lane);
-                apply_x<FAM, R>(xYp, xPm, cf, lane);
-                double t2[2] = {0.0, 0.0};
+            // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
+            const double k5 = c5 * beta;
+            const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    t2[0] += Yp[j].re * xPp[j].re + Yp[j].im * xPp[j].im;
-                    t2[1] += xYp[j].re * xPm[j].re + xYp[j].im * xPm[j].im;
-                }
-                wave_sum<2>(t2);
-                const double pp = a.w * t2[0], pm = a.w * t2[1], k5 = c5 * beta;
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    acc[j] = C(acc[j].re + k5 * ((xPp[j].re - pp * Yp[j].re) - (xPm[j].re - pm * xYp[j].re)),
-                               acc[j].im + k5 * ((xPp[j].im - pp * Yp[j].im) - (xPm[j].im - pm * xYp[j].im)));
-                }
-            }
+            for (int j = 0; j < R; ++j)
+                acc[j] = C(acc[j].re + k5 * (2.0 * kP * xrp[j].re - dpm * psi[j].re - kP * spm * rp[j].re),
+                           acc[j].im + k5 * (2.0 * kP * xrp[j].im - dpm * psi[j].im - kP * spm * rp[j].im));
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
@@ -1170,7 +1219,7 @@ static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
 template <int FAM, int R, int MODE>
 int launch_step_mode(const KArgs& a, hipStream_t st) {
-    const dim3 grid(a.n_blocks), block(256);
+    const dim3 grid(a.n_blocks), block(64 * kStepWaves<FAM, R>);
     if (MODE >= 1) {
         static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
         if (!attr_set) {
@@ -1191,6 +1240,7 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
                void* stream) {
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
+    if (kind == 4) return kStepWaves<FAM, R>;   // query: envs per step workgroup
     if (kind == 0) {
         const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2>(a, st)
                      : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1>(a, st)

@@ -198,10 +198,13 @@ KArgs base_args(const qc_handle* h) {
         }
         const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO);
         const size_t t1 = L.tf, t2 = L.tf + (size_t)(lf + lb + 2) * op.kl * op.kl * 1024;
-        int mode = t2 <= 160 * 1024 ? 2 : (t1 <= 160 * 1024 ? 1 : 0);
+        // Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
+        const size_t fx = op.fock ? (size_t)(op.R + 1) * kWave * 8 : 0;
+        int mode = t2 + fx <= 160 * 1024 ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
-        a.lds_bytes = (uint32_t)(mode == 2 ? t2 : (mode == 1 ? t1 : 0));
+        a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);
+        a.lds_bytes = mode ? (uint32_t)(a.lds_fx + fx) : 0;
     }
     a.order = nullptr;
     a.n_blocks = (uint32_t)((p.batch + h->wpb - 1) / h->wpb);

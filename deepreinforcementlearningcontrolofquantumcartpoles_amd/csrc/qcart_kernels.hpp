@@ -288,6 +288,36 @@ __device__ __forceinline__ void apply_h(const cd (&v)[R], cd (&oh)[R], const Coe
     }
 }
 
+// H v row by row: f(j, (H v)_j.re, (H v)_j.im) for j = 0..R-1 (lets a caller consume H v without
+// materialising it)
+template <int FAM, int R, typename F>
+__device__ __forceinline__ void h_rows(const cd (&v)[R], const Coef<FAM, R>& cf, int lane, F&& f) {
+    if constexpr (FAM == 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) f(j, cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
+    } else if constexpr (FAM == 1) {
+        cd e[R + 4];
+        make_ext<R, 2>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            f(j, cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re, cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
+    } else {
+        cd e[R + 8];
+        make_ext<R, 4>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+#pragma unroll
+            for (int d = 1; d <= 4; ++d) {
+                re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
+                im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
+            }
+            const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
+            f(j, in ? re : 0.0, in ? im : 0.0);
+        }
+    }
+}
+
 // H v and X v with one halo exchange
 template <int FAM, int R>
 __device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)[R], const Coef<FAM, R>& cf,
@@ -357,6 +387,31 @@ __device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF
     }
 }
 
+// u = H_F v with the force term's coefficients fx[t] = -cF X[base-1+t][base+t] (t = 0..R) read from
+// the workgroup's LDS (Fock families, tables in LDS): 8 instead of 10 FP64 ops per row
+template <int FAM, int R>
+__device__ __forceinline__ void apply_hf_fx(const cd (&v)[R], cd (&u)[R], const Coef<FAM, R>& cf, const char* fxl,
+                                            int v8, int lane) {
+    double fx[R + 1];
+#pragma unroll
+    for (int t = 0; t <= R; ++t) fx[t] = *(const double*)(fxl + t * 512 + v8);
+    if constexpr (FAM == 1) {
+        cd e[R + 4];
+        make_ext<R, 2>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            u[j] = C(cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re + fx[j + 1] * e[j + 3].re + fx[j] * e[j + 1].re,
+                     cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im + fx[j + 1] * e[j + 3].im + fx[j] * e[j + 1].im);
+    } else {
+        cd e[R + 2];
+        make_ext<R, 1>(v, e, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            u[j] = C(cf.hu[j] * v[j].re + fx[j + 1] * e[j + 2].re + fx[j] * e[j].re,
+                     cf.hu[j] * v[j].im + fx[j + 1] * e[j + 2].im + fx[j] * e[j].im);
+    }
+}
+
 // ---- counter-based noise (oracle: qo_normals)
 __device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -374,6 +429,25 @@ __device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1
         c[3] = lo0;
     }
 }
+// natural log on (0, 1] by the classic argument-reduction + Lg1..Lg7 minimax scheme (fdlibm
+// e_log.c, < 1 ulp): small and table-free, so the noise refill does not drag a constant table into
+// private memory (the library log did: ~1 GB of scratch traffic per metric launch)
+__device__ __forceinline__ double log_unit(double x) {
+    int k;
+    double m = frexp(x, &k);                       // x = m 2^k, m in [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m += m;
+        k -= 1;
+    }
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f), z = s * s, w = z * z;
+    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+    const double t2 = z * (6.666666666666735130e-01 +
+                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double Rr = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + Rr) + dk * 1.90821492927058770002e-10)) - f);
+}
+
 __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ctr, uint32_t tag, double& r0,
                                         double& r1) {
     uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), env, tag};
@@ -382,9 +456,12 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
     const uint64_t b = ((((uint64_t)c[2]) << 32) | c[3]) >> 11;
     const double u1 = ((double)a + 0.5) * 0x1.0p-53;
     const double u2 = ((double)b + 0.5) * 0x1.0p-53;
-    const double rad = sqrt(-2.0 * log(u1));
+    const double rad = sqrt(-2.0 * log_unit(u1));
+    // sin/cos(2 pi u2) as sincospi(2 u2): exact argument reduction without the large-argument
+    // (Payne-Hanek) path, so the rare noise refill stays small in registers; agrees with the oracle's
+    // libm sin/cos(2 pi u2) to ~1 ulp (the oracle rounds 2 pi u2 first)
     double s, co;
-    sincos(2.0 * M_PI * u2, &s, &co);
+    sincospi(2.0 * u2, &s, &co);
     r0 = rad * co;
     r1 = rad * s;
 }
@@ -567,7 +644,8 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        cd x = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);
+        b[j] = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);   // D^-1 y, reused by pass 2
+        cd x = b[j];
 #pragma unroll
         for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
@@ -600,7 +678,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        cd x = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);
+        cd x = b[j];
 #pragma unroll
         for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
 #pragma unroll
@@ -747,6 +825,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
     slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
     const rsrc_t rs = make_rsrc((const char*)a.tab + (size_t)slot * a.slot_bytes, SL.bytes);
     const int kf = a.kf[slot], kb = a.kb[slot];
+    const double cF = a.c * a.force[slot];
+    constexpr bool FXL = MODE >= 1 && FAM <= 1;   // H_F force coefficients from LDS (apply_hf_fx)
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
     if constexpr (MODE >= 1) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
@@ -766,6 +846,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             copy(SL.tb, SL.tf + (uint32_t)(kf + 1) * CB, (uint32_t)kb * CB);
             copy(SL.tb + 6u * CB, SL.tf + (uint32_t)(kf + 1 + kb) * CB, CB);
         }
+        if constexpr (FXL) {
+            if (threadIdx.x < 64) {
+#pragma unroll
+                for (int t = 0; t <= R; ++t) {
+                    const int r = lane * R - 1 + t;
+                    const double x = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
+                    *(double*)(img + a.lds_fx + t * 512 + lane * 8) = -cF * x;
+                }
+            }
+        }
         __syncthreads();
     }
     if (!active) return;
@@ -773,7 +863,6 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
     const int N = a.N;
     Coef<FAM, R> cf;
     load_coef<FAM, R>(cf, a, base);
-    const double cF = a.c * a.force[slot];
 
     double* gpsi = a.psi + (size_t)env * N * 2;
     cd psi[R];
@@ -858,28 +947,33 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             D1[j] = C(D1[j].im - cF * xp[j].im, -(D1[j].re - cF * xp[j].re));
         {
             cd xr[R];
+            const double gx = g4 * xbar;
             apply_x<FAM, R>(rel, xr, cf, lane);
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                D1[j] = C(D1[j].re - g4 * (xr[j].re - xbar * rel[j].re), D1[j].im - g4 * (xr[j].im - xbar * rel[j].im));
+                D1[j] = C(D1[j].re - g4 * xr[j].re + gx * rel[j].re, D1[j].im - g4 * xr[j].im + gx * rel[j].im);
         }
         QC_STAMP(1);
         {
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)
+            auto hf = [&](const cd (&v)[R], cd (&u)[R]) {
+                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb.lds + a.lds_fx, tb.v8, lane);
+                else apply_hf<FAM, R>(v, u, cF, cf, lane);
+            };
             cd t[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) t[j] = C(-a.a5 * D1[j].im, a.a5 * D1[j].re);
-            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+            hf(t, acc);
 #pragma unroll
             for (int j = 0; j < R; ++j) t[j] = C(acc[j].re - a.a4 * D1[j].re, acc[j].im - a.a4 * D1[j].im);
-            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+            hf(t, acc);
 #pragma unroll
             for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a3 * D1[j].im, acc[j].im - a.a3 * D1[j].re);
-            apply_hf<FAM, R>(t, acc, cF, cf, lane);
+            hf(t, acc);
 #pragma unroll
             for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a2 * D1[j].re, acc[j].im + a.a2 * D1[j].im);
-            apply_hf<FAM, R>(t, acc, cF, cf, lane);
-            apply_hf<FAM, R>(acc, t, cF, cf, lane);
+            hf(t, acc);
+            hf(acc, t);
             const double kA = (dW - 2.0 * c4) * beta, k2 = 2.0 * c2;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -918,68 +1012,63 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         }
         QC_STAMP(3);
         const double kY = sdt * beta, kIm = c1 - c6, kP = sdt * beta;
+        // Y+- = Y0 +- kY rel (Y+ in psi's registers) and their unnormalised means in one reduction
+        cd xYp[R];
+        double yp, ym;
         {
-            // Y- branch: Y- = Y0 - kY rel; Y+ kept in psi's registers
-            cd Ym[R], xY[R];
+            cd Ym[R], xYm[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 Ym[j] = C(psi[j].re - kY * rel[j].re, psi[j].im - kY * rel[j].im);
                 psi[j] = C(psi[j].re + kY * rel[j].re, psi[j].im + kY * rel[j].im);   // Y+
             }
-            apply_x<FAM, R>(Ym, xY, cf, lane);
-            double sm[1] = {0.0};
+            apply_x<FAM, R>(Ym, xYm, cf, lane);
+            apply_x<FAM, R>(psi, xYp, cf, lane);
+            double sm[2] = {0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < R; ++j) sm[0] += Ym[j].re * xY[j].re + Ym[j].im * xY[j].im;
-            wave_sum<1>(sm);
-            const double ym = a.w * sm[0];
-            {
-                cd hY[R];
-                apply_h<FAM, R>(Ym, hY, cf, lane);
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double hre = hY[j].re - cF * xY[j].re, him = hY[j].im - cF * xY[j].im;
-                    acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);   // -(c1-c6) (-i H_F Y-)
-                    xY[j] = C(xY[j].re - ym * Ym[j].re, xY[j].im - ym * Ym[j].im);   // rel-
-                }
+            for (int j = 0; j < R; ++j) {
+                sm[0] += psi[j].re * xYp[j].re + psi[j].im * xYp[j].im;
+                sm[1] += Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im;
             }
-            apply_x<FAM, R>(xY, Ym, cf, lane);   // X rel- (Y- no longer needed)
-            const double kRe = -(c2 - c1) * g4, kD = (c4 - c3 + c5) * beta;
+            wave_sum<2>(sm);
+            yp = a.w * sm[0];
+            ym = a.w * sm[1];
+            // Y- branch: acc -= (c1-c6) (-i H_F Y-), fused row by row with H Y- (no H Y- vector)
+            {
+                h_rows<FAM, R>(Ym, cf, lane, [&](int j, double hre, double him) {
+                    hre -= cF * xYm[j].re;
+                    him -= cF * xYm[j].im;
+                    acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);
+                    xYm[j] = C(xYm[j].re - ym * Ym[j].re, xYm[j].im - ym * Ym[j].im);   // rel-
+                });
+            }
+            apply_x<FAM, R>(xYm, Ym, cf, lane);   // X rel- (Y- no longer needed)
+            // acc += kRe (X rel- - ym rel-) + kD rel-  =  kRe X rel- + (kD - kRe ym) rel-
+            const double kRe = -(c2 - c1) * g4, kDm = (c4 - c3 + c5) * beta - kRe * ym;
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                acc[j] = C(acc[j].re + kRe * (Ym[j].re - ym * xY[j].re) + kD * xY[j].re,
-                           acc[j].im + kRe * (Ym[j].im - ym * xY[j].im) + kD * xY[j].im);
+                acc[j] = C(acc[j].re + kRe * Ym[j].re + kDm * xYm[j].re, acc[j].im + kRe * Ym[j].im + kDm * xYm[j].im);
         }
         QC_STAMP(4);
         {
             // Y+ branch (Y+ in psi); keeps X Y+, rel+ and X rel+ for the Phi means
-            cd xY[R], rp[R], xrp[R];
-            apply_x<FAM, R>(psi, xY, cf, lane);
-            double sp[1] = {0.0};
-#pragma unroll
-            for (int j = 0; j < R; ++j) sp[0] += psi[j].re * xY[j].re + psi[j].im * xY[j].im;
-            wave_sum<1>(sp);
-            const double yp = a.w * sp[0];
-            {
-                cd hY[R];
-                apply_h<FAM, R>(psi, hY, cf, lane);
-#pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    const double hre = hY[j].re - cF * xY[j].re, him = hY[j].im - cF * xY[j].im;
-                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) (-i H_F Y+)
-                    rp[j] = C(xY[j].re - yp * psi[j].re, xY[j].im - yp * psi[j].im);   // rel+
-                }
-            }
+            cd rp[R], xrp[R];
+            h_rows<FAM, R>(psi, cf, lane, [&](int j, double hre, double him) {
+                hre -= cF * xYp[j].re;
+                him -= cF * xYp[j].im;
+                acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) (-i H_F Y+)
+                rp[j] = C(xYp[j].re - yp * psi[j].re, xYp[j].im - yp * psi[j].im);   // rel+
+            });
             apply_x<FAM, R>(rp, xrp, cf, lane);
-            const double kRe = -(c1 + c2) * g4, kD = (c3 + c4 - c5) * beta;
+            const double kRe = -(c1 + c2) * g4, kDp = (c3 + c4 - c5) * beta - kRe * yp;
             QC_STAMP(5);
             // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
             //   pp/pm = yp +- w kP (<Y+, X rel+> + <rel+, X Y+>) + w kP^2 <rel+, X rel+>
             double d2[2] = {0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                acc[j] = C(acc[j].re + kRe * (xrp[j].re - yp * rp[j].re) + kD * rp[j].re,
-                           acc[j].im + kRe * (xrp[j].im - yp * rp[j].im) + kD * rp[j].im);
-                d2[0] += psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xY[j].re + rp[j].im * xY[j].im;
+                acc[j] = C(acc[j].re + kRe * xrp[j].re + kDp * rp[j].re, acc[j].im + kRe * xrp[j].im + kDp * rp[j].im);
+                d2[0] += psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xYp[j].re + rp[j].im * xYp[j].im;
                 d2[1] += rp[j].re * xrp[j].re + rp[j].im * xrp[j].im;
             }
             wave_sum<2>(d2);
@@ -987,10 +1076,11 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
             const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
+            const double fx = 2.0 * k5 * kP, fy = -k5 * dpm, fr = -k5 * kP * spm;
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                acc[j] = C(acc[j].re + k5 * (2.0 * kP * xrp[j].re - dpm * psi[j].re - kP * spm * rp[j].re),
-                           acc[j].im + k5 * (2.0 * kP * xrp[j].im - dpm * psi[j].im - kP * spm * rp[j].im));
+                acc[j] = C(acc[j].re + fx * xrp[j].re + fy * psi[j].re + fr * rp[j].re,
+                           acc[j].im + fx * xrp[j].im + fy * psi[j].im + fr * rp[j].im);
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
@@ -1020,8 +1110,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
                 xp[j] = C(xn[j].re * scale, xn[j].im * scale);
             }
             xbar = a.w * (s[1] * scale) * scale;
-            bool f = sqrt(s[2]) * scale > a.fail_thr;
-            if constexpr (FAM == 2) f = f || (sqrt(s[3]) * scale > a.fail_thr);
+            // check_boundary_error: sqrt(sum |psi|^2) > thr, compared squared (no square roots)
+            const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
+            bool f = s[2] * sc2 > thr2;
+            if constexpr (FAM == 2) f = f || (s[3] * sc2 > thr2);
             if (f && fail == 0) fail = k + 1;
             if (win_on && term < 0 && 1.0 - a.h * (s[4] * scale) * scale > 0.5) term = k + 1;
         }

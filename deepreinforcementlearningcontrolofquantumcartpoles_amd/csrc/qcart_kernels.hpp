@@ -521,11 +521,16 @@ __device__ __forceinline__ cd row_shift(cd v) {
 // then one carry of the neighbouring row's end state (row_bcast:15 upward / wave_shl + row_newbcast:15
 // downward) through the in-row prefix product P. Valid when transfer products over >= 16 lanes are
 // below kScanTol (nlev <= 4); otherwise band_solve runs the full 6-level Kogge-Stone with shuffles.
-template <int KL, bool FWD>
-__device__ __forceinline__ void scan_rows(cd (&s)[KL], const cd (&T)[4][KL * KL], const cd (&P)[KL * KL], int nlev) {
+template <int KL, bool FWD, int MODE>
+__device__ __forceinline__ void scan_rows(cd (&s)[KL], const Tab<MODE>& tb, uint32_t lv0, uint32_t lvp, int nlev) {
+    // composites are read level by level (KL = 4: 16 complex per level; all levels at once would
+    // not fit the register file), fenced for KL = 4 so the next level's reads are not hoisted
 #pragma unroll
     for (int lvl = 0; lvl < 4; ++lvl) {
         if (lvl < nlev) {
+            cd T[KL * KL];
+#pragma unroll
+            for (int e = 0; e < KL * KL; ++e) T[e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * 1024u);
             cd p[KL];
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
@@ -537,9 +542,13 @@ __device__ __forceinline__ void scan_rows(cd (&s)[KL], const cd (&T)[4][KL * KL]
 #pragma unroll
             for (int i = 0; i < KL; ++i)
 #pragma unroll
-                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], T[lvl][i * KL + k], p[k]);
+                for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], T[i * KL + k], p[k]);
+            if constexpr (KL > 2) __builtin_amdgcn_sched_barrier(0);
         }
     }
+    cd P[KL * KL];
+#pragma unroll
+    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * 1024u);
     cd c[KL];
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
@@ -556,18 +565,6 @@ __device__ __forceinline__ void scan_rows(cd (&s)[KL], const cd (&T)[4][KL * KL]
     for (int i = 0; i < KL; ++i)
 #pragma unroll
         for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], P[i * KL + k], c[k]);
-}
-
-template <int KL, int MODE>
-__device__ __forceinline__ void load_scan(cd (&T)[4][KL * KL], cd (&P)[KL * KL], const Tab<MODE>& tb, uint32_t lv0,
-                                          uint32_t lvp, int nlev) {
-#pragma unroll
-    for (int lvl = 0; lvl < 4; ++lvl)
-        if (lvl < nlev)
-#pragma unroll
-            for (int e = 0; e < KL * KL; ++e) T[lvl][e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * 1024u);
-#pragma unroll
-    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * 1024u);
 }
 
 #ifdef QCART_STAMPS
@@ -588,7 +585,6 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     const uint32_t b0 = MODE == 2 ? SL.tf + (uint32_t)(kf + 1) * CB : SL.tb;
     const uint32_t bP = MODE == 2 ? SL.tf + (uint32_t)(kf + 1 + kb) * CB : SL.tb + 6u * CB;
     const bool hf = kf <= 4, hb = kb <= 4;
-    cd T[4][KL * KL], P[KL * KL];
     // forward, pass 1 (zero incoming state): lane end state e_l
     cd s[KL];
 #pragma unroll
@@ -604,8 +600,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     }
     QC_STAMP(10);
     if (hf) {
-        load_scan<KL, MODE>(T, P, tb, f0, fP, kf);
-        scan_rows<KL, true>(s, T, P, kf);
+        scan_rows<KL, true, MODE>(s, tb, f0, fP, kf);
     } else {
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
@@ -654,8 +649,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     }
     QC_STAMP(13);
     if (hb) {
-        load_scan<KL, MODE>(T, P, tb, b0, bP, kb);
-        scan_rows<KL, false>(s, T, P, kb);
+        scan_rows<KL, false, MODE>(s, tb, b0, bP, kb);
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
@@ -803,7 +797,7 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 #define QCART_W8_MAX_R 8
 #endif
 template <int FAM, int R>
-constexpr int kStepWaves = (FAM <= 1 && R <= QCART_W8_MAX_R) ? 8 : 4;
+constexpr int kStepWaves = ((FAM <= 1 && R <= QCART_W8_MAX_R) || (FAM == 2 && R <= 3)) ? 8 : 4;
 
 template <int FAM, int R, int MODE>
 __global__ __launch_bounds__((64 * kStepWaves<FAM, R>))

@@ -797,7 +797,7 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 #define QCART_W8_MAX_R 8
 #endif
 template <int FAM, int R>
-constexpr int kStepWaves = ((FAM <= 1 && R <= QCART_W8_MAX_R) || (FAM == 2 && R <= 3)) ? 8 : 4;
+constexpr int kStepWaves = ((FAM <= 1 && R <= QCART_W8_MAX_R) || (FAM == 2 && R <= 5)) ? 8 : 4;
 
 template <int FAM, int R, int MODE>
 __global__ __launch_bounds__((64 * kStepWaves<FAM, R>))

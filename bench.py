@@ -68,9 +68,28 @@ def cpu_baseline(physics, seconds: float, threads: int):
                     n_threads=threads)
         n += chunk
     dtm = time.perf_counter() - t0
+    # single-core rate (one env on one thread, the reference's one-env-per-process model)
+    one = psi[:1].copy()
+    n1 = 0
+    t1 = time.perf_counter()
+    while time.perf_counter() - t1 < min(3.0, seconds / 4):
+        s.run_batch(one, acts[:1], physics.f_max, chunk, physics.dt, physics.gamma, seed=42, step0=n1, n_threads=1)
+        n1 += chunk
+    d1 = time.perf_counter() - t1
     return {"value": B * n / dtm, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{B} envs x {n} physics steps (N={physics.dim}, fp64, OpenMP over envs, "
-                      f"one single-threaded env per thread), {dtm:.1f} s wall"}
+                      f"one single-threaded env per thread), {dtm:.1f} s wall",
+            "single_core_value": n1 / d1, "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def latest_profile(workload: str):
@@ -181,6 +200,7 @@ def main():
                      "frac": achieved / PEAK_HBM, "traffic": None,
                      "kernel": "k_step", "kernel_ms": kern_ms,
                      "note": "achieved = 32*N B/env-step (psi read+write) x env-steps per launch / launch time"},
+        "rl_steps_per_s": value / ph.control_interval,
         "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": PEAK_FP64_VALU / 1e12,
                  "frac": flops / PEAK_FP64_VALU, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
     }

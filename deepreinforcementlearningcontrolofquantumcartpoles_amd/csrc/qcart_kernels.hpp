@@ -389,12 +389,12 @@ __device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF
 
 // u = H_F v with the force term's coefficients fx[t] = -cF X[base-1+t][base+t] (t = 0..R) read from
 // the workgroup's LDS (Fock families, tables in LDS): 8 instead of 10 FP64 ops per row
-template <int FAM, int R>
-__device__ __forceinline__ void apply_hf_fx(const cd (&v)[R], cd (&u)[R], const Coef<FAM, R>& cf, const char* fxl,
-                                            int v8, int lane) {
+template <int FAM, int R, typename TabT>
+__device__ __forceinline__ void apply_hf_fx(const cd (&v)[R], cd (&u)[R], const Coef<FAM, R>& cf, const TabT& tb,
+                                            uint32_t fx0, int lane) {
     double fx[R + 1];
 #pragma unroll
-    for (int t = 0; t <= R; ++t) fx[t] = *(const double*)(fxl + t * 512 + v8);
+    for (int t = 0; t <= R; ++t) fx[t] = *(const double*)(tb.lds + tb.v8 + fx0 + t * 512);
     if constexpr (FAM == 1) {
         cd e[R + 4];
         make_ext<R, 2>(v, e, lane);
@@ -479,21 +479,29 @@ struct Tab {
     rsrc_t rs;
     const char* lds;
     int v16, v8;   // this lane's byte offset in a 16-B / 8-B lane-interleaved run
+    int h16, h8;   // the same + 64 KiB (opaque): LDS images beyond the 16-bit ds_read offset field are
+                   // addressed from this second base with immediate offsets instead of one add per read
+    __device__ __forceinline__ const char* at16(uint32_t off) const {
+        return off < 65536u ? lds + v16 + off : lds + h16 + (off - 65536u);
+    }
+    __device__ __forceinline__ const char* at8(uint32_t off) const {
+        return off < 65536u ? lds + v8 + off : lds + h8 + (off - 65536u);
+    }
     __device__ __forceinline__ cd c(uint32_t off) const {      // lc / uc / di
         if constexpr (MODE >= 1) {
-            const double2 v = *(const double2*)(lds + off + v16);
+            const double2 v = *(const double2*)at16(off);
             return C(v.x, v.y);
         } else {
             return bld_c(rs, v16, (int)off);
         }
     }
     __device__ __forceinline__ double d(uint32_t off) const {  // m2
-        if constexpr (MODE >= 1) return *(const double*)(lds + off + v8);
+        if constexpr (MODE >= 1) return *(const double*)at8(off);
         else return bld_d(rs, v8, (int)off);
     }
     __device__ __forceinline__ cd comp(uint32_t off) const {   // scan composites
         if constexpr (MODE == 2) {
-            const double2 v = *(const double2*)(lds + off + v16);
+            const double2 v = *(const double2*)(lds + v16 + off);
             return C(v.x, v.y);
         } else {
             return bld_c(rs, v16, (int)off);
@@ -918,9 +926,9 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         }
         // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
         // reads and their addresses inside the step (LICM would otherwise pin them in registers)
-        int lane_o = lane;
-        asm volatile("" : "+v"(lane_o));
-        const Tab<MODE> tb{rs, (const char*)smem_dyn, lane_o * 16, lane_o * 8};
+        int lane_o = lane, h16 = lane * 16 + 65536, h8 = lane * 8 + 65536;
+        asm volatile("" : "+v"(lane_o), "+v"(h16), "+v"(h8));
+        const Tab<MODE> tb{rs, (const char*)smem_dyn, lane_o * 16, lane_o * 8, h16, h8};
         const double c1 = 0.5 * inv_sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 * inv_sdt * (dW * dW - dt);
         const double c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
         const double c6 = 0.25 * sdt * dW;
@@ -951,7 +959,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         {
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)
             auto hf = [&](const cd (&v)[R], cd (&u)[R]) {
-                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb.lds + a.lds_fx, tb.v8, lane);
+                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lane);
                 else apply_hf<FAM, R>(v, u, cF, cf, lane);
             };
             cd t[R];
@@ -1084,19 +1092,30 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         {
             cd xn[R];
             apply_x<FAM, R>(acc, xn, cf, lane);
-            double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            // full reductions only for the norm and the next <x>; the boundary sums (Fail) touch the
+            // few lanes holding the edge rows and are read from them directly
+            double s[2] = {0.0, 0.0}, ptop = 0.0, pbot = 0.0, pwin = 0.0;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 const double p2 = acc[j].re * acc[j].re + acc[j].im * acc[j].im;
                 s[0] += p2;
                 s[1] += acc[j].re * xn[j].re + acc[j].im * xn[j].im;
                 const int r = base + j;
-                if (r >= N - a.bnd_len && r < N) s[2] += p2;
-                if (r < a.bnd_len) s[3] += p2;
-                if (r >= a.win_lo && r < a.win_hi) s[4] += p2;
+                if (r >= N - a.bnd_len && r < N) ptop += p2;
+                if constexpr (FAM == 2) {
+                    if (r < a.bnd_len) pbot += p2;
+                    if (r >= a.win_lo && r < a.win_hi) pwin += p2;
+                }
             }
-            wave_sum<5>(s);
-            double scale = 1.0 / sqrt(s[0]);
+            wave_sum<2>(s);
+            double stop = 0.0, sbot = 0.0;
+            for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
+            if constexpr (FAM == 2)
+                for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
+            // 1/sqrt(s0): hardware estimate + two Newton steps (full fp64 precision)
+            double scale = __builtin_amdgcn_rsq(s[0]);
+            scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
+            scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
             if constexpr (FAM == 2) scale = scale * a.inv_sqrt_w;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -1106,10 +1125,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             xbar = a.w * (s[1] * scale) * scale;
             // check_boundary_error: sqrt(sum |psi|^2) > thr, compared squared (no square roots)
             const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
-            bool f = s[2] * sc2 > thr2;
-            if constexpr (FAM == 2) f = f || (s[3] * sc2 > thr2);
+            bool f = stop * sc2 > thr2;
+            if constexpr (FAM == 2) f = f || (sbot * sc2 > thr2);
             if (f && fail == 0) fail = k + 1;
-            if (win_on && term < 0 && 1.0 - a.h * (s[4] * scale) * scale > 0.5) term = k + 1;
+            if constexpr (FAM == 2) {
+                if (win_on && term < 0) {
+                    double sw[1] = {pwin};
+                    wave_sum<1>(sw);
+                    if (1.0 - a.h * (sw[0] * scale) * scale > 0.5) term = k + 1;
+                }
+            }
         }
     }
 #ifdef QCART_STAMPS

@@ -56,6 +56,7 @@ CASES = {
     "ho71": cfg.DEFAULTS[cfg.HO],
     "qo171": cfg.DEFAULTS[cfg.QO],
     "iqo513": cfg.DEFAULTS[cfg.IQO].with_(x_max=12.8),
+    "qo1025": cfg.BENCH_CONFIGS["C3"]["physics"],          # C3 grid: x_n = 1025 (R = 17)
 }
 
 
@@ -122,7 +123,7 @@ def run_pair(oracle_mod, ph, steps, B, act_lo, act_hi, chunk=80, seed=7, policy=
     ("iho64", 1000, 8, "random"), ("iho181", 1000, 8, "random"), ("iho512_g05", 1000, 8, "pd"),
     ("iho512", 1000, 8, "random"), ("iho512_exact_g05", 1000, 4, "pd"),
     ("ho256", 1000, 6, "random"), ("ho71", 1000, 8, "random"), ("qo171", 1000, 6, "random"),
-    ("iqo513", 1000, 4, "random"),
+    ("iqo513", 1000, 4, "random"), ("qo1025", 1000, 3, "random"),
 ])
 def test_psi_parity_injected_noise(oracle_mod, name, steps, B, policy):
     """||psi_GPU - psi_ref||_2 < 1e-9 after 1000 steps (fp64) for every env whose trajectory stays
@@ -345,3 +346,38 @@ def test_table_placements_bitwise_equal(monkeypatch, case):
     st1.step(y, acts[5:6], 40)
     torch.cuda.synchronize()
     assert torch.equal(y[0], outs[0][5])
+
+
+@pytest.mark.parametrize("config", ["C2", "C4"])
+def test_config_size_batch_properties(oracle_mod, config):
+    """At a BASELINE config's full per-GPU batch (C2: IHO N=512 B=4096; C4: IQO x_n=513, B=8192 per GPU
+    of its 8-GPU run): every env stays normalised, the call is deterministic, and sampled envs of the
+    big batch match the oracle run alone with the same in-kernel Philox stream (1e-10 over 80 steps)."""
+    conf = cfg.BENCH_CONFIGS[config]
+    ph = conf["physics"]
+    B = conf["batch"] if config == "C2" else conf["batch"] // 8
+    st = Stepper(ph, B, 0, seed=99)
+    psi = st.new_state()
+    if ph.fock:
+        st.reset(psi, 1, arg0=16)
+    else:
+        st.reset(psi, 2, arg0=0.0, arg1=0.0, arg2=1.0)
+    psi0 = psi.clone()
+    acts = torch.randint(0, 21, (B,), generator=torch.Generator(device="cuda").manual_seed(5),
+                         device="cuda", dtype=torch.int32)
+    st.step(psi, acts, 80)
+    st.step_counter = 0
+    again = psi0.clone()
+    st.step(again, acts, 80)
+    torch.cuda.synchronize()
+    assert torch.equal(psi, again)
+    w = 1.0 if ph.fock else ph.grid_size
+    norms = (psi.abs() ** 2).sum(1) * w
+    assert float((norms - 1).abs().max()) < 1e-12
+    osys = oracle_sys(oracle_mod, ph)
+    for e in (0, 1, B // 2, B - 1):
+        ref = psi0[e:e + 1].cpu().numpy().copy()
+        osys.run_batch(ref, acts[e:e + 1].cpu().numpy(), ph.f_max, 80, ph.dt, ph.gamma, seed=99, env_offset=e,
+                       n_threads=1)
+        err = wnorm(ph, psi[e].cpu().numpy() - ref[0])
+        assert err < 1e-10, (e, err)

@@ -4,7 +4,7 @@ PKG := deepreinforcementlearningcontrolofquantumcartpoles_amd
 CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
-OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_group.o qcart_dispatch.o qcart_api.o qcart_tables.o)
+OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_dispatch.o qcart_api.o qcart_tables.o)
 HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
 all: $(LIB) oracle
@@ -14,6 +14,8 @@ all: $(LIB) oracle
 KFLAGS ?= -mllvm -disable-machine-licm
 # (the grid TU keeps LICM: its 9-band loop-invariant addressing is worth hoisting, measured +12 %)
 $(CSRC)/build/qcart_k_grid.o: KFLAGS :=
+# fp32 TU: no SLP packing (v_pk_fma_f32 pairs cost more register shuffles than they save here)
+$(CSRC)/build/qcart_k_f32.o: KFLAGS += -fno-slp-vectorize
 $(CSRC)/build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c $< -o $@

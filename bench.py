@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 FLOPS_PER_ELEM = {0: 350, 1: 470, 2: 705, 3: 705}
 PEAK_HBM = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 PEAK_FP64_VALU = 78.6e12   # MI355X FP64 vector (spec)
+PEAK_FP32_VALU = 157.3e12  # MI355X FP32 vector (spec; config C5 computes in fp32)
 
 
 def parse():
@@ -177,7 +178,10 @@ def main():
     value = units / elapsed
     N = ph.dim
     per_launch_units = B * n_sub
-    achieved = 32.0 * N * per_launch_units / (kern_ms * 1e-3)
+    fp32 = ph.precision == 1
+    bpe = 16.0 if fp32 else 32.0             # psi read + write per element: complex64 / complex128
+    peak_valu = PEAK_FP32_VALU if fp32 else PEAK_FP64_VALU
+    achieved = bpe * N * per_launch_units / (kern_ms * 1e-3)
     flops = FLOPS_PER_ELEM[ph.family] * N * per_launch_units / (kern_ms * 1e-3)
     res = {
         "metric": "env-steps/sec (whole node), inverted-harmonic grid=512 batch=65536; 1/2/4/8 GPU",
@@ -190,7 +194,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f32" if fp32 else "f64",
         "data": "synthetic (random psi0 on Fock levels < 16; actions ~ U{0..20} per control step)",
         "config": {"workload": f"{cfg.FAMILY_NAMES[ph.family]} N={N} per-GPU batch={B} "
                                f"{n_sub} physics steps + moments per step ({args.config})",
@@ -199,10 +203,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": None,
                      "kernel": "k_step", "kernel_ms": kern_ms,
-                     "note": "achieved = 32*N B/env-step (psi read+write) x env-steps per launch / launch time"},
+                     "note": f"achieved = {int(bpe)}*N B/env-step (psi read+write) x env-steps per launch / launch time"},
         "rl_steps_per_s": value / ph.control_interval,
-        "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": PEAK_FP64_VALU / 1e12,
-                 "frac": flops / PEAK_FP64_VALU, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
+        "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": peak_valu / 1e12,
+                 "frac": flops / peak_valu, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
     }
     # HBM traffic per launch measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, tools/prof_summary.py)
     # for this same workload, when a committed profile exists
@@ -210,7 +214,7 @@ def main():
     if prof is not None:
         res["roofline"]["traffic"] = prof["hbm_bytes_per_launch"]
         res["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC, profiles/%s_summary.json)" % prof["tag"]
-        res["roofline"]["algorithmic_bytes_per_launch"] = 32.0 * N * per_launch_units
+        res["roofline"]["algorithmic_bytes_per_launch"] = bpe * N * per_launch_units
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(ph, args.cpu_seconds, args.cpu_threads)

@@ -45,7 +45,7 @@ class QcParams(ctypes.Structure):
         ("dt", ctypes.c_double),
         ("f_max", ctypes.c_double),
         ("n_actions", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("precision", ctypes.c_int32),   # 0 fp64, 1 fp32 (Fock families; complex64 states)
         ("batch", ctypes.c_int64),
         ("env_offset", ctypes.c_int64),
         ("seed", ctypes.c_uint64),

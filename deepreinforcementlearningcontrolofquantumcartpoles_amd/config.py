@@ -28,6 +28,7 @@ class Physics:
     f_max: float = 5.0          # convert_to_force spacing F_max / 10 (IHO/RL.py:107-111)
     n_actions: int = 21
     a_mode: int = 0             # 0 = reference MKL descriptor semantics, 1 = exact A
+    precision: int = 0          # 0 = fp64 (the reference's), 1 = fp32 (config C5; Fock families)
 
     @property
     def dt(self) -> float:
@@ -93,6 +94,6 @@ BENCH_CONFIGS = {
     "C2": dict(physics=DEFAULTS[IHO].with_(n_max=511), batch=4096),
     "C3": dict(physics=DEFAULTS[QO].with_(x_max=8.5, grid_size=8.5 / 512), batch=16384),
     "C4": dict(physics=DEFAULTS[IQO].with_(x_max=12.8, grid_size=0.05), batch=65536),
-    "C5": dict(physics=DEFAULTS[IHO].with_(n_max=2047), batch=262144),
+    "C5": dict(physics=DEFAULTS[IHO].with_(n_max=2047, precision=1), batch=262144),
     "metric": dict(physics=DEFAULTS[IHO].with_(n_max=511), batch=65536),
 }

@@ -41,6 +41,7 @@ class Stepper:
         p.mass = physics.mass
         p.moment_order = physics.moment_order
         p.a_mode = physics.a_mode
+        p.precision = physics.precision
         p.gamma = physics.gamma
         p.dt = physics.dt
         p.f_max = physics.f_max
@@ -74,9 +75,14 @@ class Stepper:
         s = torch.cuda.current_stream(self.device).cuda_stream
         L.check(L.lib().qc_set_stream(self._h, ctypes.c_void_p(s)), self._h)
 
+    @property
+    def state_dtype(self) -> torch.dtype:
+        return torch.complex64 if self.physics.precision == 1 else torch.complex128
+
     def _check_psi(self, psi: torch.Tensor):
-        if psi.dtype != torch.complex128:
-            raise ValueError("The state array does not match the required datatype: Complex128")
+        if psi.dtype != self.state_dtype:
+            name = "Complex64" if self.physics.precision == 1 else "Complex128"
+            raise ValueError("The state array does not match the required datatype: " + name)
         if psi.dim() != 2 or psi.shape[1] != self.N or psi.shape[0] != self.batch:
             raise ValueError(f"The state array does not match the required size ({self.batch}, {self.N})")
         if psi.device != self.device or not psi.is_contiguous():
@@ -84,7 +90,7 @@ class Stepper:
 
     # ------------------------------------------------------------------ state helpers
     def new_state(self) -> torch.Tensor:
-        return torch.zeros((self.batch, self.N), dtype=torch.complex128, device=self.device)
+        return torch.zeros((self.batch, self.N), dtype=self.state_dtype, device=self.device)
 
     def set_seed(self, seed: int):
         L.check(L.lib().qc_set_seed(self._h, seed), self._h)

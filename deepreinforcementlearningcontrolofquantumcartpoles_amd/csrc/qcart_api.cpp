@@ -75,13 +75,18 @@ int hip_check(qc_handle* h, hipError_t e, const char* what) {
 }
 
 // the rows-per-lane instantiations compiled in qcart_kernels.hip
-int pick_R(int family, int N) {
+int pick_R(int family, int N, int precision) {
     static const int r_fock_ho[] = {1, 2, 4, 8};
     static const int r_fock_iho[] = {1, 2, 3, 4, 8, 16};
     static const int r_grid[] = {1, 2, 3, 5, 9, 17};
+    static const int r_f32_ho[] = {4, 8, 32}, r_f32_iho[] = {8, 16, 32};
     const int need = (N + kWave - 1) / kWave;
     const int* list = family == QC_HO ? r_fock_ho : (family == QC_IHO ? r_fock_iho : r_grid);
-    const int n = family == QC_HO ? 4 : 6;
+    int n = family == QC_HO ? 4 : 6;
+    if (precision == QC_FP32) {
+        list = family == QC_HO ? r_f32_ho : r_f32_iho;
+        n = 3;
+    }
     for (int i = 0; i < n; i++)
         if (list[i] >= need) return list[i];
     return -1;
@@ -110,20 +115,24 @@ int upload(qc_handle* h, T** dst, const T* src, size_t n) {
 // (slot capacity kMaxSlots)
 int upload_tables(qc_handle* h) {
     const int Np = h->op.Npad, kl = h->op.kl, R = h->op.R;
-    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO);
+    const bool f32 = h->p.precision == QC_FP32;   // fp32 blocks: the fp64 factors rounded once
+    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u);
     h->slot_bytes = L.bytes;
-    const size_t sd = L.bytes / 8;   // doubles per slot
-    std::vector<double> tab((size_t)kMaxSlots * sd, 0.0), force(kMaxSlots, 0.0);
+    std::vector<uint8_t> tab((size_t)kMaxSlots * L.bytes, 0);
+    std::vector<double> force(kMaxSlots, 0.0);
     std::vector<int32_t> kf(kMaxSlots, 0), kb(kMaxSlots, 0);
     auto ilv = [&](int b, int r) { return ((size_t)b * R + (r % R)) * kWave + r / R; };   // row-band element
-    auto put = [&](double* base, uint32_t off, size_t elem, cplx v) {
-        double* q = base + off / 8 + elem * 2;
-        q[0] = v.real();
-        q[1] = v.imag();
+    auto putr = [&](uint8_t* blk, uint32_t off, size_t elem, double v) {
+        if (f32) ((float*)(blk + off))[elem] = (float)v;
+        else ((double*)(blk + off))[elem] = v;
+    };
+    auto put = [&](uint8_t* blk, uint32_t off, size_t elem, cplx v) {
+        putr(blk, off, 2 * elem, v.real());
+        putr(blk, off, 2 * elem + 1, v.imag());
     };
     for (size_t s = 0; s < h->acts.size(); s++) {
         const ActHost& a = h->acts[s];
-        double* blk = tab.data() + s * sd;
+        uint8_t* blk = tab.data() + s * L.bytes;
         for (int b = 0; b < kl; b++)
             for (int r = 0; r < Np; r++) {
                 put(blk, L.lc, ilv(b, r), a.lc[(size_t)b * Np + r]);
@@ -132,7 +141,7 @@ int upload_tables(qc_handle* h) {
         for (int r = 0; r < Np; r++) put(blk, L.di, ilv(0, r), a.dinv[r]);
         if (h->op.family == QC_IHO)
             for (int b = 0; b < kMirrorBands; b++)
-                for (int r = 0; r < Np; r++) blk[L.m2 / 8 + ilv(b, r)] = a.m2[(size_t)b * Np + r];
+                for (int r = 0; r < Np; r++) putr(blk, L.m2, ilv(b, r), a.m2[(size_t)b * Np + r]);
         const size_t kk = (size_t)kl * kl;
         for (int v = 0; v < kTabLevels; v++)
             for (int l = 0; l < kWave; l++)
@@ -146,7 +155,7 @@ int upload_tables(qc_handle* h) {
         kb[s] = a.kb;
     }
     int rc;
-    if ((rc = upload(h, &h->d_tab, tab.data(), tab.size()))) return rc;
+    if ((rc = upload(h, &h->d_tab, (const double*)tab.data(), tab.size() / 8))) return rc;
     if ((rc = upload(h, &h->d_force, force.data(), force.size()))) return rc;
     if ((rc = upload(h, &h->d_kf, kf.data(), kf.size()))) return rc;
     if ((rc = upload(h, &h->d_kb, kb.data(), kb.size()))) return rc;
@@ -196,16 +205,19 @@ KArgs base_args(const qc_handle* h) {
             lf = std::max(lf, s.kf);
             lb = std::max(lb, s.kb);
         }
-        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO);
-        const size_t t1 = L.tf, t2 = L.tf + (size_t)(lf + lb + 2) * op.kl * op.kl * 1024;
-        // Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
-        const size_t fx = op.fock ? (size_t)(op.R + 1) * kWave * 8 : 0;
+        const bool f32 = p.precision == QC_FP32;
+        const uint32_t es = f32 ? 8u : 16u;   // bytes per complex table element
+        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO, es);
+        const size_t t1 = L.tf, t2 = L.tf + (size_t)(lf + lb + 2) * op.kl * op.kl * kWave * es;
+        // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
+        const size_t fx = (op.fock && !f32) ? (size_t)(op.R + 1) * kWave * 8 : 0;
         int mode = t2 + fx <= 160 * 1024 ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
         a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);
         a.lds_bytes = mode ? (uint32_t)(a.lds_fx + fx) : 0;
     }
+    a.precision = p.precision;
     a.order = nullptr;
     a.n_blocks = (uint32_t)((p.batch + h->wpb - 1) / h->wpb);
     a.n_obs = qc_n_obs(h);
@@ -253,6 +265,8 @@ int validate_params(const qc_params* p, std::string& err) {
         return QC_EINVAL;
     }
     if (p->a_mode != QC_A_REFERENCE && p->a_mode != QC_A_EXACT) { err = "bad a_mode"; return QC_EINVAL; }
+    if (p->precision != QC_FP64 && p->precision != QC_FP32) { err = "precision must be 0 (fp64) or 1 (fp32)"; return QC_EINVAL; }
+    if (p->precision == QC_FP32 && p->family >= QC_QO) { err = "fp32 is built for the Fock families only"; return QC_EINVAL; }
     return QC_OK;
 }
 
@@ -288,13 +302,13 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     OpHost probe;
     rc = build_ops(p->family, p->n_max, p->omega, p->x_max, p->grid_size, p->lambda_, p->mass, 1 << 12, probe, err);
     if (rc) { set_create_err(err); delete h; return rc; }
-    h->R = pick_R(p->family, probe.N);
-    if (h->R < 0 || !have_kernel(p->family, h->R)) {
+    h->R = pick_R(p->family, probe.N, p->precision);
+    if (h->R < 0 || !have_kernel(p->family, h->R, p->precision)) {
         set_create_err("no kernel instantiated for N = " + std::to_string(probe.N));
         delete h;
         return QC_ENOTBUILT;
     }
-    h->wpb = step_waves(p->family, h->R);
+    h->wpb = step_waves(p->family, h->R, p->precision);
     if (h->wpb <= 0) {
         set_create_err("no step kernel for N = " + std::to_string(probe.N));
         delete h;

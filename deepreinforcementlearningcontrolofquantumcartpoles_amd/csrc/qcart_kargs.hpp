@@ -17,21 +17,22 @@ namespace qcart {
 struct SlotLayout {
     uint32_t lc, uc, di, m2, tf, tb, bytes;
 };
-constexpr SlotLayout slot_layout(int kl, int R, bool has_m2) {
+// es: bytes of one complex element (16 fp64, 8 fp32); real bands use es / 2
+constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16) {
     SlotLayout L{};
     L.lc = 0;
-    L.uc = L.lc + 16u * 64u * (uint32_t)(kl * R);
-    L.di = L.uc + 16u * 64u * (uint32_t)(kl * R);
-    L.m2 = L.di + 16u * 64u * (uint32_t)R;
-    L.tf = L.m2 + (has_m2 ? 8u * 64u * 10u * (uint32_t)R : 0u);
-    L.tb = L.tf + 16u * 64u * 7u * (uint32_t)(kl * kl);
-    L.bytes = L.tb + 16u * 64u * 7u * (uint32_t)(kl * kl);
+    L.uc = L.lc + es * 64u * (uint32_t)(kl * R);
+    L.di = L.uc + es * 64u * (uint32_t)(kl * R);
+    L.m2 = L.di + es * 64u * (uint32_t)R;
+    L.tf = L.m2 + (has_m2 ? (es / 2) * 64u * 10u * (uint32_t)R : 0u);
+    L.tb = L.tf + es * 64u * 7u * (uint32_t)(kl * kl);
+    L.bytes = L.tb + es * 64u * 7u * (uint32_t)(kl * kl);
     return L;
 }
 
 struct KArgs {
     // state and I/O (device pointers)
-    double* psi;               // [B][N] complex interleaved
+    void* psi;                 // [B][N] complex interleaved, fp64 or fp32 (precision)
     const int32_t* actions;    // [B] or null
     const int32_t* env_steps;  // [B] per-env step budget (min with n_steps) or null
     const double* noise;       // [n_steps][B][2] or null
@@ -54,6 +55,7 @@ struct KArgs {
     int32_t win_lo, win_hi;    // IQO outside-probability window [lo, hi); win_hi <= win_lo: off
     int32_t moment_order;
     int32_t n_obs;
+    int32_t precision;         // 0 fp64, 1 fp32 (psi storage and step arithmetic)
     int32_t tab_mode;          // step kernel factor tables: 0 global, 1 LDS (lc/uc/di/m2), 2 + composites
     uint32_t lds_bytes;        // dynamic LDS per block for tab_mode >= 1
     uint32_t lds_fx;           // LDS offset of the H_F force coefficients (Fock, tab_mode >= 1)
@@ -77,14 +79,15 @@ struct KArgs {
 };
 
 // host-side launchers (qcart_kernels.hip)
+// (the kernel precision is a.precision)
 int launch_step(int family, int R, const KArgs& a, void* stream);
 int launch_obs(int family, int R, const KArgs& a, void* stream);   // moments into obs_out
 int launch_aux(int family, int R, int what, const KArgs& a, double xth, void* out, void* stream);
 int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mask, double a0,
                  double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                  void* stream);
-bool have_kernel(int family, int R);
-int step_waves(int family, int R);   // envs (waves) per step-kernel workgroup
+bool have_kernel(int family, int R, int precision = 0);
+int step_waves(int family, int R, int precision = 0);   // envs (waves) per step-kernel workgroup
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
 int launch_group(const int32_t* actions, int64_t B, int n_slots, int gran, int32_t* order, int32_t cap,
                  void* stream);

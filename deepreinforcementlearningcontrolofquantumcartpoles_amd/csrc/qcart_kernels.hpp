@@ -23,23 +23,34 @@
 
 namespace qcart {
 
-struct cd {
-    double re, im;
+// Complex values of the working precision RT: double (the reference's fp64; every config but C5) or
+// float (C5's fp32 path, Fock families only).
+template <typename RT>
+struct cx {
+    RT re, im;
 };
-__device__ __forceinline__ cd C(double r, double i) {
-    cd c;
+using cd = cx<double>;
+template <typename RT>
+__device__ __forceinline__ cx<RT> C(RT r, RT i) {
+    cx<RT> c;
     c.re = r;
     c.im = i;
     return c;
 }
-__device__ __forceinline__ cd cmul(cd a, cd b) { return C(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re); }
-__device__ __forceinline__ cd cmac(cd acc, cd a, cd b) {   // acc + a*b
+template <typename RT>
+__device__ __forceinline__ cx<RT> cmul(cx<RT> a, cx<RT> b) {
+    return C(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
+}
+template <typename RT>
+__device__ __forceinline__ cx<RT> cmac(cx<RT> acc, cx<RT> a, cx<RT> b) {   // acc + a*b
     return C(acc.re + a.re * b.re - a.im * b.im, acc.im + a.re * b.im + a.im * b.re);
 }
-__device__ __forceinline__ cd cmsub(cd acc, cd a, cd b) {  // acc - a*b
+template <typename RT>
+__device__ __forceinline__ cx<RT> cmsub(cx<RT> acc, cx<RT> a, cx<RT> b) {  // acc - a*b
     return C(acc.re - (a.re * b.re - a.im * b.im), acc.im - (a.re * b.im + a.im * b.re));
 }
-__device__ __forceinline__ cd ld(const double* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
+template <typename RT>
+__device__ __forceinline__ cx<RT> ld(const RT* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
 // Factor-block reads: one buffer descriptor per slot block (SGPRs), per-lane VGPR offset, constant
 // SGPR / immediate byte offsets. Out-of-range reads return 0 (descriptor bounds = block size).
 using rsrc_t = __amdgpu_buffer_rsrc_t;
@@ -50,16 +61,29 @@ __device__ __forceinline__ double u2d(unsigned lo, unsigned hi) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 #ifdef QCART_EXPT_NOLOAD   // latency experiment only: results are wrong
-__device__ __forceinline__ cd bld_c(rsrc_t, int voff, int soff) { return C(1e-3 * (double)((voff + soff) & 7), 1e-4); }
-__device__ __forceinline__ double bld_d(rsrc_t, int voff, int soff) { return 1e-6 * (double)((voff + soff) & 7); }
+template <typename RT>
+__device__ __forceinline__ cx<RT> bld_c(rsrc_t, int voff, int soff) { return C(RT(1e-3) * (RT)((voff + soff) & 7), RT(1e-4)); }
+template <typename RT>
+__device__ __forceinline__ RT bld_d(rsrc_t, int voff, int soff) { return RT(1e-6) * (RT)((voff + soff) & 7); }
 #else
-__device__ __forceinline__ cd bld_c(rsrc_t r, int voff, int soff) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-    return C(u2d(v[0], v[1]), u2d(v[2], v[3]));
+template <typename RT>
+__device__ __forceinline__ cx<RT> bld_c(rsrc_t r, int voff, int soff) {
+    if constexpr (sizeof(RT) == 8) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+        return C(u2d(v[0], v[1]), u2d(v[2], v[3]));
+    } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+        return C(__uint_as_float(v[0]), __uint_as_float(v[1]));
+    }
 }
-__device__ __forceinline__ double bld_d(rsrc_t r, int voff, int soff) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-    return u2d(v[0], v[1]);
+template <typename RT>
+__device__ __forceinline__ RT bld_d(rsrc_t r, int voff, int soff) {
+    if constexpr (sizeof(RT) == 8) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+        return u2d(v[0], v[1]);
+    } else {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+    }
 }
 #endif
 
@@ -89,6 +113,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+__device__ __forceinline__ float readlane_d(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 
 // ---- cross-lane primitives (VALU only: DPP and v_permlane*_swap, no LDS round trip)
 // dst lane i <- src lane (i -/+ 1); a lane whose source is outside the wave reads 0 (bound_ctrl)
@@ -99,15 +126,21 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
-__device__ __forceinline__ double shr1(double v) { return dpp_d<0x138>(v); }   // wave_shr:1
-__device__ __forceinline__ double shl1(double v) { return dpp_d<0x130>(v); }   // wave_shl:1
-template <int D>
-__device__ __forceinline__ double shr(double v) {
+template <int CTRL>
+__device__ __forceinline__ float dpp_d(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+template <typename RT>
+__device__ __forceinline__ RT shr1(RT v) { return dpp_d<0x138>(v); }   // wave_shr:1
+template <typename RT>
+__device__ __forceinline__ RT shl1(RT v) { return dpp_d<0x130>(v); }   // wave_shl:1
+template <int D, typename RT>
+__device__ __forceinline__ RT shr(RT v) {
     if constexpr (D == 0) return v;
     else return shr<D - 1>(shr1(v));
 }
-template <int D>
-__device__ __forceinline__ double shl(double v) {
+template <int D, typename RT>
+__device__ __forceinline__ RT shl(RT v) {
     if constexpr (D == 0) return v;
     else return shl<D - 1>(shl1(v));
 }
@@ -127,9 +160,17 @@ __device__ __forceinline__ double add_swap32(double v) {
     const auto b = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
     return mk_d(a[0], b[0]) + mk_d(a[1], b[1]);
 }
+__device__ __forceinline__ float add_swap16(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float add_swap32(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
 // all-lane sum; every pairing is symmetric, so every lane ends with bit-identical values
-template <int NV>
-__device__ __forceinline__ void wave_sum(double (&v)[NV]) {
+template <int NV, typename RT>
+__device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0xb1>(v[i]);    // quad_perm [1,0,3,2]
 #pragma unroll
@@ -157,8 +198,8 @@ struct Fam<2> { static constexpr int KL = 4; };
 // ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t.
 // Lanes outside the wave read 0 (the operators have zero rows there). dl is compile-time: the shift
 // by dl lanes is dl chained DPP wave shifts.
-template <int R, int H>
-__device__ __forceinline__ void make_ext(const cd (&v)[R], cd (&e)[R + 2 * H], int lane) {
+template <int R, int H, typename RT>
+__device__ __forceinline__ void make_ext(const cx<RT> (&v)[R], cx<RT> (&e)[R + 2 * H], int lane) {
 #pragma unroll
     for (int j = 0; j < R; ++j) e[H + j] = v[j];
 #pragma unroll
@@ -183,8 +224,8 @@ __device__ __forceinline__ void make_ext(const cd (&v)[R], cd (&e)[R + 2 * H], i
     }
 }
 // lower halo only: e[t] = row base - H + t, t < H (up to 10 rows: dl <= 10 lanes for R = 1)
-template <int R, int H>
-__device__ __forceinline__ void make_lo(const cd (&v)[R], cd (&e)[H], int lane) {
+template <int R, int H, typename RT>
+__device__ __forceinline__ void make_lo(const cx<RT> (&v)[R], cx<RT> (&e)[H], int lane) {
 #pragma unroll
     for (int t = 0; t < H; ++t) {
         const int o = H - t;
@@ -196,57 +237,57 @@ __device__ __forceinline__ void make_lo(const cd (&v)[R], cd (&e)[H], int lane) 
             else if (dl == 3) e[t] = C(shr<3>(v[idx].re), shr<3>(v[idx].im));
             else e[t] = C(shr<4>(v[idx].re), shr<4>(v[idx].im));
         } else {
-            double re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
+            RT re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
             const bool ok = lane >= dl;
-            e[t] = C(ok ? re : 0.0, ok ? im : 0.0);
+            e[t] = C(ok ? re : RT(0), ok ? im : RT(0));
         }
     }
 }
 
 // ---- per-lane operator coefficients (action independent), loaded once per call
-template <int FAM, int R>
+template <int FAM, int R, typename RT = double>
 struct Coef {
-    double xu[R + 1];  // Fock: X[base-1+t][base+t]
-    double hu[R + 2];  // IHO: H[base-2+t][base+t]; HO / grid: H[base+t][base+t]
-    double xg[R];      // grid: x_{base+t}
+    RT xu[R + 1];  // Fock: X[base-1+t][base+t]
+    RT hu[R + 2];  // IHO: H[base-2+t][base+t]; HO / grid: H[base+t][base+t]
+    RT xg[R];      // grid: x_{base+t}
     int base, N;
-    double hoff[5];
+    RT hoff[5];
 };
 
-template <int FAM, int R>
-__device__ __forceinline__ void load_coef(Coef<FAM, R>& cf, const KArgs& a, int base) {
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void load_coef(Coef<FAM, R, RT>& cf, const KArgs& a, int base) {
     cf.base = base;
     cf.N = a.N;
     if constexpr (FAM <= 1) {
 #pragma unroll
         for (int t = 0; t <= R; ++t) {
             int r = base - 1 + t;
-            cf.xu[t] = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
+            cf.xu[t] = (r >= 0 && r < a.Npad) ? (RT)a.xu[r] : RT(0);
         }
     }
     if constexpr (FAM == 1) {
 #pragma unroll
         for (int t = 0; t < R + 2; ++t) {
             int r = base - 2 + t;
-            cf.hu[t] = (r >= 0 && r < a.Npad) ? a.hu[r] : 0.0;
+            cf.hu[t] = (r >= 0 && r < a.Npad) ? (RT)a.hu[r] : RT(0);
         }
     } else {
 #pragma unroll
-        for (int t = 0; t < R; ++t) cf.hu[t] = a.hu[base + t];
+        for (int t = 0; t < R; ++t) cf.hu[t] = (RT)a.hu[base + t];
     }
     if constexpr (FAM == 2) {
 #pragma unroll
-        for (int t = 0; t < R; ++t) cf.xg[t] = a.xg[base + t];
+        for (int t = 0; t < R; ++t) cf.xg[t] = (RT)a.xg[base + t];
 #pragma unroll
-        for (int d = 0; d < 5; ++d) cf.hoff[d] = a.hoff[d];
+        for (int d = 0; d < 5; ++d) cf.hoff[d] = (RT)a.hoff[d];
     }
 }
 
 // X v   (IHO/simulation_i.cpp:168-196 Fock tridiagonal; QO/simulation_quart.cpp:214-229 grid diag)
-template <int FAM, int R>
-__device__ __forceinline__ void apply_x(const cd (&v)[R], cd (&o)[R], const Coef<FAM, R>& cf, int lane) {
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void apply_x(const cx<RT> (&v)[R], cx<RT> (&o)[R], const Coef<FAM, R, RT>& cf, int lane) {
     if constexpr (FAM <= 1) {
-        cd e[R + 2];
+        cx<RT> e[R + 2];
         make_ext<R, 1>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -260,74 +301,74 @@ __device__ __forceinline__ void apply_x(const cd (&v)[R], cd (&o)[R], const Coef
 
 // H v (the force-free Hamiltonian; IHO/simulation_i.cpp:75-99, HO/simulation.cpp:69-80, QO/simulation_quart.cpp:
 // 40-58)
-template <int FAM, int R>
-__device__ __forceinline__ void apply_h(const cd (&v)[R], cd (&oh)[R], const Coef<FAM, R>& cf, int lane) {
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void apply_h(const cx<RT> (&v)[R], cx<RT> (&oh)[R], const Coef<FAM, R, RT>& cf, int lane) {
     if constexpr (FAM == 0) {
 #pragma unroll
         for (int j = 0; j < R; ++j) oh[j] = C(cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
     } else if constexpr (FAM == 1) {
-        cd e[R + 4];
+        cx<RT> e[R + 4];
         make_ext<R, 2>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j)
             oh[j] = C(cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re, cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
     } else {
-        cd e[R + 8];
+        cx<RT> e[R + 8];
         make_ext<R, 4>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+            RT re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
 #pragma unroll
             for (int d = 1; d <= 4; ++d) {
                 re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
                 im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
             }
             const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
-            oh[j] = C(in ? re : 0.0, in ? im : 0.0);
+            oh[j] = C(in ? re : RT(0), in ? im : RT(0));
         }
     }
 }
 
 // H v row by row: f(j, (H v)_j.re, (H v)_j.im) for j = 0..R-1 (lets a caller consume H v without
 // materialising it)
-template <int FAM, int R, typename F>
-__device__ __forceinline__ void h_rows(const cd (&v)[R], const Coef<FAM, R>& cf, int lane, F&& f) {
+template <int FAM, int R, typename RT, typename F>
+__device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, RT>& cf, int lane, F&& f) {
     if constexpr (FAM == 0) {
 #pragma unroll
         for (int j = 0; j < R; ++j) f(j, cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
     } else if constexpr (FAM == 1) {
-        cd e[R + 4];
+        cx<RT> e[R + 4];
         make_ext<R, 2>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j)
             f(j, cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re, cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
     } else {
-        cd e[R + 8];
+        cx<RT> e[R + 8];
         make_ext<R, 4>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+            RT re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
 #pragma unroll
             for (int d = 1; d <= 4; ++d) {
                 re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
                 im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
             }
             const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
-            f(j, in ? re : 0.0, in ? im : 0.0);
+            f(j, in ? re : RT(0), in ? im : RT(0));
         }
     }
 }
 
 // H v and X v with one halo exchange
-template <int FAM, int R>
-__device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)[R], const Coef<FAM, R>& cf,
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void apply_hx(const cx<RT> (&v)[R], cx<RT> (&oh)[R], cx<RT> (&ox)[R], const Coef<FAM, R, RT>& cf,
                                          int lane) {
     if constexpr (FAM == 0) {
         apply_x<FAM, R>(v, ox, cf, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) oh[j] = C(cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
     } else if constexpr (FAM == 1) {
-        cd e[R + 4];
+        cx<RT> e[R + 4];
         make_ext<R, 2>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -337,50 +378,50 @@ __device__ __forceinline__ void apply_hx(const cd (&v)[R], cd (&oh)[R], cd (&ox)
                       cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im);
         }
     } else {
-        cd e[R + 8];
+        cx<RT> e[R + 8];
         make_ext<R, 4>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             ox[j] = C(cf.xg[j] * v[j].re, cf.xg[j] * v[j].im);
-            double re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
+            RT re = cf.hu[j] * v[j].re, im = cf.hu[j] * v[j].im;
 #pragma unroll
             for (int d = 1; d <= 4; ++d) {
                 re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
                 im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
             }
             const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
-            oh[j] = C(in ? re : 0.0, in ? im : 0.0);
+            oh[j] = C(in ? re : RT(0), in ? im : RT(0));
         }
     }
 }
 
 // u = H_F v = H v - cF X v
-template <int FAM, int R>
-__device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF, const Coef<FAM, R>& cf,
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void apply_hf(const cx<RT> (&v)[R], cx<RT> (&u)[R], RT cF, const Coef<FAM, R, RT>& cf,
                                          int lane) {
     // fused per row (no full-length H v / X v temporaries: keeps the step within 256 VGPRs)
     if constexpr (FAM == 1) {
-        cd e[R + 4];
+        cx<RT> e[R + 4];
         make_ext<R, 2>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const double hre = cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re;
-            const double him = cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im;
-            const double xre = cf.xu[j + 1] * e[j + 3].re + cf.xu[j] * e[j + 1].re;
-            const double xim = cf.xu[j + 1] * e[j + 3].im + cf.xu[j] * e[j + 1].im;
+            const RT hre = cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re;
+            const RT him = cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im;
+            const RT xre = cf.xu[j + 1] * e[j + 3].re + cf.xu[j] * e[j + 1].re;
+            const RT xim = cf.xu[j + 1] * e[j + 3].im + cf.xu[j] * e[j + 1].im;
             u[j] = C(hre - cF * xre, him - cF * xim);
         }
     } else if constexpr (FAM == 0) {
-        cd e[R + 2];
+        cx<RT> e[R + 2];
         make_ext<R, 1>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const double xre = cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re;
-            const double xim = cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im;
+            const RT xre = cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re;
+            const RT xim = cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im;
             u[j] = C(cf.hu[j] * v[j].re - cF * xre, cf.hu[j] * v[j].im - cF * xim);
         }
     } else {
-        cd hx[R], xx[R];
+        cx<RT> hx[R], xx[R];
         apply_hx<FAM, R>(v, hx, xx, cf, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j) u[j] = C(hx[j].re - cF * xx[j].re, hx[j].im - cF * xx[j].im);
@@ -389,21 +430,21 @@ __device__ __forceinline__ void apply_hf(const cd (&v)[R], cd (&u)[R], double cF
 
 // u = H_F v with the force term's coefficients fx[t] = -cF X[base-1+t][base+t] (t = 0..R) read from
 // the workgroup's LDS (Fock families, tables in LDS): 8 instead of 10 FP64 ops per row
-template <int FAM, int R, typename TabT>
-__device__ __forceinline__ void apply_hf_fx(const cd (&v)[R], cd (&u)[R], const Coef<FAM, R>& cf, const TabT& tb,
+template <int FAM, int R, typename RT, typename TabT>
+__device__ __forceinline__ void apply_hf_fx(const cx<RT> (&v)[R], cx<RT> (&u)[R], const Coef<FAM, R, RT>& cf, const TabT& tb,
                                             uint32_t fx0, int lane) {
-    double fx[R + 1];
+    RT fx[R + 1];
 #pragma unroll
-    for (int t = 0; t <= R; ++t) fx[t] = *(const double*)(tb.lds + tb.v8 + fx0 + t * 512);
+    for (int t = 0; t <= R; ++t) fx[t] = *(const RT*)(tb.lds + tb.vr + fx0 + t * 64 * (int)sizeof(RT));
     if constexpr (FAM == 1) {
-        cd e[R + 4];
+        cx<RT> e[R + 4];
         make_ext<R, 2>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j)
             u[j] = C(cf.hu[j + 2] * e[j + 4].re + cf.hu[j] * e[j].re + fx[j + 1] * e[j + 3].re + fx[j] * e[j + 1].re,
                      cf.hu[j + 2] * e[j + 4].im + cf.hu[j] * e[j].im + fx[j + 1] * e[j + 3].im + fx[j] * e[j + 1].im);
     } else {
-        cd e[R + 2];
+        cx<RT> e[R + 2];
         make_ext<R, 1>(v, e, lane);
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -474,38 +515,39 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
 // (buffer loads); MODE 1: lc/uc/di/m2 from the workgroup's shared LDS image of its slot's block;
 // MODE 2: the scan composites too. The LDS image is the block's first SL.tf bytes verbatim,
 // followed by the kept forward levels, the row prefix, the kept backward levels and the row suffix.
-template <int MODE>
+template <int MODE, typename RT>
 struct Tab {
     rsrc_t rs;
     const char* lds;
-    int v16, v8;   // this lane's byte offset in a 16-B / 8-B lane-interleaved run
-    int h16, h8;   // the same + 64 KiB (opaque): LDS images beyond the 16-bit ds_read offset field are
+    int vc, vr;    // this lane's byte offset in a complex / real lane-interleaved run
+    int hc, hr;    // the same + 64 KiB (opaque): LDS images beyond the 16-bit ds_read offset field are
                    // addressed from this second base with immediate offsets instead of one add per read
-    __device__ __forceinline__ const char* at16(uint32_t off) const {
-        return off < 65536u ? lds + v16 + off : lds + h16 + (off - 65536u);
+    __device__ __forceinline__ const char* atc(uint32_t off) const {
+        return off < 65536u ? lds + vc + off : lds + hc + (off - 65536u);
     }
-    __device__ __forceinline__ const char* at8(uint32_t off) const {
-        return off < 65536u ? lds + v8 + off : lds + h8 + (off - 65536u);
+    __device__ __forceinline__ const char* atr(uint32_t off) const {
+        return off < 65536u ? lds + vr + off : lds + hr + (off - 65536u);
     }
-    __device__ __forceinline__ cd c(uint32_t off) const {      // lc / uc / di
-        if constexpr (MODE >= 1) {
-            const double2 v = *(const double2*)at16(off);
+    __device__ __forceinline__ static cx<RT> lds_c(const char* p) {
+        if constexpr (sizeof(RT) == 8) {
+            const double2 v = *(const double2*)p;
             return C(v.x, v.y);
         } else {
-            return bld_c(rs, v16, (int)off);
-        }
-    }
-    __device__ __forceinline__ double d(uint32_t off) const {  // m2
-        if constexpr (MODE >= 1) return *(const double*)at8(off);
-        else return bld_d(rs, v8, (int)off);
-    }
-    __device__ __forceinline__ cd comp(uint32_t off) const {   // scan composites
-        if constexpr (MODE == 2) {
-            const double2 v = *(const double2*)(lds + v16 + off);
+            const float2 v = *(const float2*)p;
             return C(v.x, v.y);
-        } else {
-            return bld_c(rs, v16, (int)off);
         }
+    }
+    __device__ __forceinline__ cx<RT> c(uint32_t off) const {      // lc / uc / di
+        if constexpr (MODE >= 1) return lds_c(atc(off));
+        else return bld_c<RT>(rs, vc, (int)off);
+    }
+    __device__ __forceinline__ RT d(uint32_t off) const {          // m2
+        if constexpr (MODE >= 1) return *(const RT*)atr(off);
+        else return bld_d<RT>(rs, vr, (int)off);
+    }
+    __device__ __forceinline__ cx<RT> comp(uint32_t off) const {   // scan composites
+        if constexpr (MODE == 2) return lds_c(lds + vc + off);
+        else return bld_c<RT>(rs, vc, (int)off);
     }
 };
 
@@ -517,9 +559,13 @@ __device__ __forceinline__ double dpp_dm(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
     return mk_d((unsigned)lo, (unsigned)hi);
 }
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_dm(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+}
 // in-row shifts (16-lane DPP rows; sources outside the row read 0)
-template <int D, bool UP>
-__device__ __forceinline__ cd row_shift(cd v) {
+template <int D, bool UP, typename RT>
+__device__ __forceinline__ cx<RT> row_shift(cx<RT> v) {
     constexpr int CTRL = UP ? (0x110 + D) : (0x100 + D);   // row_shr:D / row_shl:D
     return C(dpp_d<CTRL>(v.re), dpp_d<CTRL>(v.im));
 }
@@ -529,17 +575,19 @@ __device__ __forceinline__ cd row_shift(cd v) {
 // then one carry of the neighbouring row's end state (row_bcast:15 upward / wave_shl + row_newbcast:15
 // downward) through the in-row prefix product P. Valid when transfer products over >= 16 lanes are
 // below kScanTol (nlev <= 4); otherwise band_solve runs the full 6-level Kogge-Stone with shuffles.
-template <int KL, bool FWD, int MODE>
-__device__ __forceinline__ void scan_rows(cd (&s)[KL], const Tab<MODE>& tb, uint32_t lv0, uint32_t lvp, int nlev) {
+template <int KL, bool FWD, int MODE, typename RT>
+__device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& tb, uint32_t lv0, uint32_t lvp,
+                                          int nlev) {
+    constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
     // composites are read level by level (KL = 4: 16 complex per level; all levels at once would
     // not fit the register file), fenced for KL = 4 so the next level's reads are not hoisted
 #pragma unroll
     for (int lvl = 0; lvl < 4; ++lvl) {
         if (lvl < nlev) {
-            cd T[KL * KL];
+            cx<RT> T[KL * KL];
 #pragma unroll
-            for (int e = 0; e < KL * KL; ++e) T[e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * 1024u);
-            cd p[KL];
+            for (int e = 0; e < KL * KL; ++e) T[e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * CE);
+            cx<RT> p[KL];
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
                 if (lvl == 0) p[k] = row_shift<1, FWD>(s[k]);
@@ -554,10 +602,10 @@ __device__ __forceinline__ void scan_rows(cd (&s)[KL], const Tab<MODE>& tb, uint
             if constexpr (KL > 2) __builtin_amdgcn_sched_barrier(0);
         }
     }
-    cd P[KL * KL];
+    cx<RT> P[KL * KL];
 #pragma unroll
-    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * 1024u);
-    cd c[KL];
+    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * CE);
+    cx<RT> c[KL];
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
         if constexpr (FWD) {
@@ -565,7 +613,7 @@ __device__ __forceinline__ void scan_rows(cd (&s)[KL], const Tab<MODE>& tb, uint
             c[k] = C(dpp_dm<0x142, 0xe>(s[k].re), dpp_dm<0x142, 0xe>(s[k].im));
         } else {
             // first lane of row r+1 -> lane 15 of row r (wave_shl:1) -> every lane of row r
-            const cd t = C(shl1(s[k].re), shl1(s[k].im));
+            const cx<RT> t = C(shl1(s[k].re), shl1(s[k].im));
             c[k] = C(dpp_dm<0x15F, 0xf>(t.re), dpp_dm<0x15F, 0xf>(t.im));
         }
     }
@@ -584,24 +632,25 @@ __device__ __forceinline__ void scan_rows(cd (&s)[KL], const Tab<MODE>& tb, uint
 #endif
 // Composite level offsets: forward level l at f0 + l*C, row prefix at fP; backward at b0 + l*C, bP
 // (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
-template <int KL, int R, int MODE, bool M2>
-__device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int kf, int kb,
+template <int KL, int R, int MODE, bool M2, typename RT>
+__device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& tb, int kf, int kb,
                                            int lane QC_SOLVE_STAMP_ARGS) {
-    constexpr SlotLayout SL = slot_layout(KL, R, M2);
-    constexpr uint32_t CB = KL * KL * 1024u;
+    constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
+    constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>));
+    constexpr uint32_t CB = KL * KL * CE;
     const uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + (uint32_t)kf * CB : SL.tf + 6u * CB;
     const uint32_t b0 = MODE == 2 ? SL.tf + (uint32_t)(kf + 1) * CB : SL.tb;
     const uint32_t bP = MODE == 2 ? SL.tf + (uint32_t)(kf + 1 + kb) * CB : SL.tb + 6u * CB;
     const bool hf = kf <= 4, hb = kb <= 4;
     // forward, pass 1 (zero incoming state): lane end state e_l
-    cd s[KL];
+    cx<RT> s[KL];
 #pragma unroll
-    for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
+    for (int k = 0; k < KL; ++k) s[k] = C(RT(0), RT(0));
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        cd y = b[j];
+        cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * 1024u), s[k]);
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
@@ -613,7 +662,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
             const int d = 1 << lvl;
-            cd p[KL];
+            cx<RT> p[KL];
 #pragma unroll
             for (int k = 0; k < KL; ++k)
                 p[k] = (lvl == 0) ? C(shr1(s[k].re), shr1(s[k].im))
@@ -623,7 +672,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
                 for (int i = 0; i < KL; ++i)
 #pragma unroll
                     for (int k = 0; k < KL; ++k)
-                        s[i] = cmac(s[i], tb.comp(f0 + (uint32_t)(lvl * KL * KL + i * KL + k) * 1024u), p[k]);
+                        s[i] = cmac(s[i], tb.comp(f0 + (uint32_t)(lvl * KL * KL + i * KL + k) * CE), p[k]);
             }
         }
     }
@@ -633,9 +682,9 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        cd y = b[j];
+        cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * 1024u), s[k]);
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
@@ -644,13 +693,13 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     QC_STAMP(12);
     // backward, pass 1 (rows high -> low): x_r = dinv_r y_r - sum_k uc_k x_{r+k}
 #pragma unroll
-    for (int k = 0; k < KL; ++k) s[k] = C(0.0, 0.0);
+    for (int k = 0; k < KL; ++k) s[k] = C(RT(0), RT(0));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        b[j] = cmul(tb.c(SL.di + (uint32_t)j * 1024u), b[j]);   // D^-1 y, reused by pass 2
-        cd x = b[j];
+        b[j] = cmul(tb.c(SL.di + (uint32_t)j * CE), b[j]);   // D^-1 y, reused by pass 2
+        cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -661,7 +710,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
-            cd p[KL];
+            cx<RT> p[KL];
 #pragma unroll
             for (int k = 0; k < KL; ++k)
                 p[k] = (lvl == 0) ? C(shl1(s[k].re), shl1(s[k].im))
@@ -671,7 +720,7 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
                 for (int i = 0; i < KL; ++i)
 #pragma unroll
                     for (int k = 0; k < KL; ++k)
-                        s[i] = cmac(s[i], tb.comp(b0 + (uint32_t)(lvl * KL * KL + i * KL + k) * 1024u), p[k]);
+                        s[i] = cmac(s[i], tb.comp(b0 + (uint32_t)(lvl * KL * KL + i * KL + k) * CE), p[k]);
             }
         }
     }
@@ -680,9 +729,9 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
-        cd x = b[j];
+        cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * 1024u), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -693,22 +742,23 @@ __device__ __forceinline__ void band_solve(cd (&b)[R], const Tab<MODE>& tb, int 
 // ---- observations ---------------------------------------------------------------------------
 // Fock 'xp' (IHO/main_parallel.py:129-131): [<x>, <p>, <x^2>-<x>^2, <p^2>-<p>^2, <xp+px>/2-<x><p>]
 // with the truncated operators: <x^2> = |X psi|^2, <p^2> = |P psi|^2, <xp+px>/2 = Re<X psi, P psi>.
-template <int FAM, int R>
-__device__ __forceinline__ void fock_obs(const cd (&psi)[R], const Coef<FAM, R>& cf, int lane, double (&o)[5]) {
-    cd e[R + 2];
+template <int FAM, int R, typename RT>
+__device__ __forceinline__ void fock_obs(const cx<RT> (&psi)[R], const Coef<FAM, R, RT>& cf, int lane,
+                                         double (&o)[5]) {
+    cx<RT> e[R + 2];
     make_ext<R, 1>(psi, e, lane);
-    double s[5] = {0, 0, 0, 0, 0};
+    double s[5] = {0, 0, 0, 0, 0};   // sums in fp64 at either working precision
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const cd xp = C(cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re, cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im);
+        const cx<RT> xp = C(cf.xu[j + 1] * e[j + 2].re + cf.xu[j] * e[j].re, cf.xu[j + 1] * e[j + 2].im + cf.xu[j] * e[j].im);
         // P psi = i (xu[r-1] psi_{r-1} - xu[r] psi_{r+1})
-        const cd t = C(cf.xu[j] * e[j].re - cf.xu[j + 1] * e[j + 2].re, cf.xu[j] * e[j].im - cf.xu[j + 1] * e[j + 2].im);
-        const cd pp = C(-t.im, t.re);
-        s[0] += psi[j].re * xp.re + psi[j].im * xp.im;
-        s[1] += psi[j].re * pp.re + psi[j].im * pp.im;
-        s[2] += xp.re * xp.re + xp.im * xp.im;
-        s[3] += pp.re * pp.re + pp.im * pp.im;
-        s[4] += xp.re * pp.re + xp.im * pp.im;
+        const cx<RT> t = C(cf.xu[j] * e[j].re - cf.xu[j + 1] * e[j + 2].re, cf.xu[j] * e[j].im - cf.xu[j + 1] * e[j + 2].im);
+        const cx<RT> pp = C(-t.im, t.re);
+        s[0] += (double)(psi[j].re * xp.re + psi[j].im * xp.im);
+        s[1] += (double)(psi[j].re * pp.re + psi[j].im * pp.im);
+        s[2] += (double)(xp.re * xp.re + xp.im * xp.im);
+        s[3] += (double)(pp.re * pp.re + pp.im * pp.im);
+        s[4] += (double)(xp.re * pp.re + xp.im * pp.im);
     }
     wave_sum<5>(s);
     o[0] = s[0];
@@ -804,15 +854,19 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 #ifndef QCART_W8_MAX_R
 #define QCART_W8_MAX_R 8
 #endif
-template <int FAM, int R>
-constexpr int kStepWaves = ((FAM <= 1 && R <= QCART_W8_MAX_R) || (FAM == 2 && R <= 5)) ? 8 : 4;
+// (fp32 rows take half the registers: R_eff = R * sizeof(RT) / 8)
+template <int FAM, int R, typename RT = double>
+constexpr int kStepWaves =
+    ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= 5)) ? 8 : 4;
 
-template <int FAM, int R, int MODE>
-__global__ __launch_bounds__((64 * kStepWaves<FAM, R>))
-__attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R> / 4)))) void k_step(const KArgs a) {
+template <int FAM, int R, int MODE, typename RT = double>
+__global__ __launch_bounds__((64 * kStepWaves<FAM, R, RT>))
+__attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM, R, RT> / 4)))) void k_step(
+    const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
-    constexpr int W = kStepWaves<FAM, R>;
-    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1);
+    constexpr int W = kStepWaves<FAM, R, RT>;
+    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>));
+    constexpr uint32_t CE = 64u * sizeof(cx<RT>), CR = 64u * sizeof(RT);   // lane-run bytes
     const int lane = threadIdx.x & 63;
     // env of this wave: a.order (envs grouped by force slot, W per block, -1 = idle) or identity
     const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * W] : (int64_t)blockIdx.x * W;
@@ -827,8 +881,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
     slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
     const rsrc_t rs = make_rsrc((const char*)a.tab + (size_t)slot * a.slot_bytes, SL.bytes);
     const int kf = a.kf[slot], kb = a.kb[slot];
-    const double cF = a.c * a.force[slot];
-    constexpr bool FXL = MODE >= 1 && FAM <= 1;   // H_F force coefficients from LDS (apply_hf_fx)
+    const double cFd = a.c * a.force[slot];
+    const RT cF = (RT)cFd;
+    // H_F force coefficients from LDS (apply_hf_fx): fp64 Fock families with the tables in LDS
+    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8;
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
     if constexpr (MODE >= 1) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
@@ -842,7 +898,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         };
         copy(0, 0, SL.tf);
         if constexpr (MODE == 2) {
-            constexpr uint32_t CB = KL * KL * 1024u;
+            constexpr uint32_t CB = KL * KL * CE;
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
             copy(SL.tf + 6u * CB, SL.tf + (uint32_t)kf * CB, CB);
             copy(SL.tb, SL.tf + (uint32_t)(kf + 1) * CB, (uint32_t)kb * CB);
@@ -854,7 +910,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
                 for (int t = 0; t <= R; ++t) {
                     const int r = lane * R - 1 + t;
                     const double x = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
-                    *(double*)(img + a.lds_fx + t * 512 + lane * 8) = -cF * x;
+                    *(double*)(img + a.lds_fx + t * 512 + lane * 8) = -cFd * x;
                 }
             }
         }
@@ -863,33 +919,35 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
     if (!active) return;
     const int base = lane * R;
     const int N = a.N;
-    Coef<FAM, R> cf;
+    Coef<FAM, R, RT> cf;
     load_coef<FAM, R>(cf, a, base);
 
-    double* gpsi = a.psi + (size_t)env * N * 2;
-    cd psi[R];
+    RT* gpsi = (RT*)a.psi + (size_t)env * N * 2;
+    cx<RT> psi[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(RT(0), RT(0));
 
     const bool win_on = a.win_hi > a.win_lo;
-    cd xp[R];
+    cx<RT> xp[R];
     apply_x<FAM, R>(psi, xp, cf, lane);
-    double xbar;
+    RT xbar;
     int term = -1, fail = 0;
     {
         double s[2] = {0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            s[0] += psi[j].re * xp[j].re + psi[j].im * xp[j].im;
+            s[0] += (double)(psi[j].re * xp[j].re + psi[j].im * xp[j].im);
             const int r = base + j;
-            if (r >= a.win_lo && r < a.win_hi) s[1] += psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+            if (r >= a.win_lo && r < a.win_hi) s[1] += (double)(psi[j].re * psi[j].re + psi[j].im * psi[j].im);
         }
         wave_sum<2>(s);
-        xbar = a.w * s[0];                                        // x_expct (IHO:197-203, QO:230-236)
+        xbar = (RT)(a.w * s[0]);                                  // x_expct (IHO:197-203, QO:230-236)
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
     const double inv_sdt = 1.0 / sdt, inv_dt = 1.0 / dt;
+    // vector-facing constants at the working precision
+    const RT g4r = (RT)g4, dtr = (RT)dt, a2r = (RT)a.a2, a3r = (RT)a.a3, a4r = (RT)a.a4, a5r = (RT)a.a5;
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
@@ -921,14 +979,15 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
         if (lane == 0) {
-            if (a.q_out) a.q_out[(size_t)k * a.B + env] = xbar + dW * a.inv_sqrt2g * inv_dt;
-            if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = xbar;
+            if (a.q_out) a.q_out[(size_t)k * a.B + env] = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
+            if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = (double)xbar;
         }
         // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
         // reads and their addresses inside the step (LICM would otherwise pin them in registers)
-        int lane_o = lane, h16 = lane * 16 + 65536, h8 = lane * 8 + 65536;
-        asm volatile("" : "+v"(lane_o), "+v"(h16), "+v"(h8));
-        const Tab<MODE> tb{rs, (const char*)smem_dyn, lane_o * 16, lane_o * 8, h16, h8};
+        constexpr int EC = (int)sizeof(cx<RT>), ER = (int)sizeof(RT);
+        int lane_o = lane, hc = lane * EC + 65536, hr = lane * ER + 65536;
+        asm volatile("" : "+v"(lane_o), "+v"(hc), "+v"(hr));
+        const Tab<MODE, RT> tb{rs, (const char*)smem_dyn, lane_o * EC, lane_o * ER, hc, hr};
         const double c1 = 0.5 * inv_sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 * inv_sdt * (dW * dW - dt);
         const double c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
         const double c6 = 0.25 * sdt * dW;
@@ -940,7 +999,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         //   C  acc = psi + kA rel + k2 D1 + u + mirror(D1);  psi <- Y0 = psi + dt D1
         //   D  Y- branch, then Y+ branch (D1ImRe IHO:301-318, D2 IHO:320-333)
         //   E  Phi+- means from <Y+, X rel+> products (no X Phi+- applications)
-        cd acc[R], rel[R], D1[R];
+        cx<RT> acc[R], rel[R], D1[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
         apply_h<FAM, R>(psi, D1, cf, lane);
@@ -948,40 +1007,40 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         for (int j = 0; j < R; ++j)   // D1 = -i (H psi - cF X psi)
             D1[j] = C(D1[j].im - cF * xp[j].im, -(D1[j].re - cF * xp[j].re));
         {
-            cd xr[R];
-            const double gx = g4 * xbar;
+            cx<RT> xr[R];
+            const RT gx = g4r * xbar;
             apply_x<FAM, R>(rel, xr, cf, lane);
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                D1[j] = C(D1[j].re - g4 * xr[j].re + gx * rel[j].re, D1[j].im - g4 * xr[j].im + gx * rel[j].im);
+                D1[j] = C(D1[j].re - g4r * xr[j].re + gx * rel[j].re, D1[j].im - g4r * xr[j].im + gx * rel[j].im);
         }
         QC_STAMP(1);
         {
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)
-            auto hf = [&](const cd (&v)[R], cd (&u)[R]) {
+            auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
                 if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lane);
                 else apply_hf<FAM, R>(v, u, cF, cf, lane);
             };
-            cd t[R];
+            cx<RT> t[R];
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(-a.a5 * D1[j].im, a.a5 * D1[j].re);
+            for (int j = 0; j < R; ++j) t[j] = C(-a5r * D1[j].im, a5r * D1[j].re);
             hf(t, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re - a.a4 * D1[j].re, acc[j].im - a.a4 * D1[j].im);
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re - a4r * D1[j].re, acc[j].im - a4r * D1[j].im);
             hf(t, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a3 * D1[j].im, acc[j].im - a.a3 * D1[j].re);
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a3r * D1[j].im, acc[j].im - a3r * D1[j].re);
             hf(t, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a.a2 * D1[j].re, acc[j].im + a.a2 * D1[j].im);
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a2r * D1[j].re, acc[j].im + a2r * D1[j].im);
             hf(t, acc);
             hf(acc, t);
-            const double kA = (dW - 2.0 * c4) * beta, k2 = 2.0 * c2;
+            const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2);
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re + t[j].re,
                            psi[j].im + kA * rel[j].im + k2 * D1[j].im + t[j].im);
-                psi[j] = C(psi[j].re + dt * D1[j].re, psi[j].im + dt * D1[j].im);   // Y0
+                psi[j] = C(psi[j].re + dtr * D1[j].re, psi[j].im + dtr * D1[j].im);   // Y0
             }
         }
         QC_STAMP(2);
@@ -990,22 +1049,22 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             // reads go in batches of MB bands fenced from the arithmetic so each batch is in flight at once
             if (a.mirror) {
                 constexpr int MB = 1;
-                cd lo[10];
+                cx<RT> lo[10];
                 make_lo<R, 10>(D1, lo, lane);
 #pragma unroll
                 for (int h = 0; h < 10 / MB; ++h) {
-                    double mv[MB][R];
+                    RT mv[MB][R];
 #pragma unroll
                     for (int dd = 0; dd < MB; ++dd)
 #pragma unroll
-                        for (int j = 0; j < R; ++j) mv[dd][j] = tb.d(SL.m2 + (uint32_t)((MB * h + dd) * R + j) * 512u);
+                        for (int j = 0; j < R; ++j) mv[dd][j] = tb.d(SL.m2 + (uint32_t)((MB * h + dd) * R + j) * CR);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int j = 0; j < R; ++j)
 #pragma unroll
                         for (int dd = 0; dd < MB; ++dd) {
                             const int d = MB * h + dd + 1;
-                            const cd dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
+                            const cx<RT> dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
                                                        : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
                             acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
                         }
@@ -1013,12 +1072,13 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             }
         }
         QC_STAMP(3);
-        const double kY = sdt * beta, kIm = c1 - c6, kP = sdt * beta;
+        const RT kY = (RT)(sdt * beta), kIm = (RT)(c1 - c6);
+        const double kP = sdt * beta;
         // Y+- = Y0 +- kY rel (Y+ in psi's registers) and their unnormalised means in one reduction
-        cd xYp[R];
+        cx<RT> xYp[R];
         double yp, ym;
         {
-            cd Ym[R], xYm[R];
+            cx<RT> Ym[R], xYm[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 Ym[j] = C(psi[j].re - kY * rel[j].re, psi[j].im - kY * rel[j].im);
@@ -1029,24 +1089,26 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             double sm[2] = {0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                sm[0] += psi[j].re * xYp[j].re + psi[j].im * xYp[j].im;
-                sm[1] += Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im;
+                sm[0] += (double)(psi[j].re * xYp[j].re + psi[j].im * xYp[j].im);
+                sm[1] += (double)(Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im);
             }
             wave_sum<2>(sm);
             yp = a.w * sm[0];
             ym = a.w * sm[1];
+            const RT ymr = (RT)ym;
             // Y- branch: acc -= (c1-c6) (-i H_F Y-), fused row by row with H Y- (no H Y- vector)
             {
-                h_rows<FAM, R>(Ym, cf, lane, [&](int j, double hre, double him) {
+                h_rows<FAM, R>(Ym, cf, lane, [&](int j, RT hre, RT him) {
                     hre -= cF * xYm[j].re;
                     him -= cF * xYm[j].im;
                     acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);
-                    xYm[j] = C(xYm[j].re - ym * Ym[j].re, xYm[j].im - ym * Ym[j].im);   // rel-
+                    xYm[j] = C(xYm[j].re - ymr * Ym[j].re, xYm[j].im - ymr * Ym[j].im);   // rel-
                 });
             }
             apply_x<FAM, R>(xYm, Ym, cf, lane);   // X rel- (Y- no longer needed)
             // acc += kRe (X rel- - ym rel-) + kD rel-  =  kRe X rel- + (kD - kRe ym) rel-
-            const double kRe = -(c2 - c1) * g4, kDm = (c4 - c3 + c5) * beta - kRe * ym;
+            const double kRed = -(c2 - c1) * g4;
+            const RT kRe = (RT)kRed, kDm = (RT)((c4 - c3 + c5) * beta - kRed * ym);
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 acc[j] = C(acc[j].re + kRe * Ym[j].re + kDm * xYm[j].re, acc[j].im + kRe * Ym[j].im + kDm * xYm[j].im);
@@ -1054,15 +1116,17 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         QC_STAMP(4);
         {
             // Y+ branch (Y+ in psi); keeps X Y+, rel+ and X rel+ for the Phi means
-            cd rp[R], xrp[R];
-            h_rows<FAM, R>(psi, cf, lane, [&](int j, double hre, double him) {
+            cx<RT> rp[R], xrp[R];
+            const RT ypr = (RT)yp;
+            h_rows<FAM, R>(psi, cf, lane, [&](int j, RT hre, RT him) {
                 hre -= cF * xYp[j].re;
                 him -= cF * xYp[j].im;
                 acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) (-i H_F Y+)
-                rp[j] = C(xYp[j].re - yp * psi[j].re, xYp[j].im - yp * psi[j].im);   // rel+
+                rp[j] = C(xYp[j].re - ypr * psi[j].re, xYp[j].im - ypr * psi[j].im);   // rel+
             });
             apply_x<FAM, R>(rp, xrp, cf, lane);
-            const double kRe = -(c1 + c2) * g4, kDp = (c3 + c4 - c5) * beta - kRe * yp;
+            const double kRed = -(c1 + c2) * g4;
+            const RT kRe = (RT)kRed, kDp = (RT)((c3 + c4 - c5) * beta - kRed * yp);
             QC_STAMP(5);
             // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
             //   pp/pm = yp +- w kP (<Y+, X rel+> + <rel+, X Y+>) + w kP^2 <rel+, X rel+>
@@ -1070,15 +1134,15 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 acc[j] = C(acc[j].re + kRe * xrp[j].re + kDp * rp[j].re, acc[j].im + kRe * xrp[j].im + kDp * rp[j].im);
-                d2[0] += psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xYp[j].re + rp[j].im * xYp[j].im;
-                d2[1] += rp[j].re * xrp[j].re + rp[j].im * xrp[j].im;
+                d2[0] += (double)(psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xYp[j].re + rp[j].im * xYp[j].im);
+                d2[1] += (double)(rp[j].re * xrp[j].re + rp[j].im * xrp[j].im);
             }
             wave_sum<2>(d2);
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
             const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
-            const double fx = 2.0 * k5 * kP, fy = -k5 * dpm, fr = -k5 * kP * spm;
+            const RT fx = (RT)(2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(-k5 * kP * spm);
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 acc[j] = C(acc[j].re + fx * xrp[j].re + fy * psi[j].re + fr * rp[j].re,
@@ -1090,16 +1154,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
         QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
-            cd xn[R];
+            cx<RT> xn[R];
             apply_x<FAM, R>(acc, xn, cf, lane);
             // full reductions only for the norm and the next <x>; the boundary sums (Fail) touch the
             // few lanes holding the edge rows and are read from them directly
             double s[2] = {0.0, 0.0}, ptop = 0.0, pbot = 0.0, pwin = 0.0;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const double p2 = acc[j].re * acc[j].re + acc[j].im * acc[j].im;
+                const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
                 s[0] += p2;
-                s[1] += acc[j].re * xn[j].re + acc[j].im * xn[j].im;
+                s[1] += (double)(acc[j].re * xn[j].re + acc[j].im * xn[j].im);
                 const int r = base + j;
                 if (r >= N - a.bnd_len && r < N) ptop += p2;
                 if constexpr (FAM == 2) {
@@ -1119,10 +1183,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
             if constexpr (FAM == 2) scale = scale * a.inv_sqrt_w;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                psi[j] = C(acc[j].re * scale, acc[j].im * scale);
-                xp[j] = C(xn[j].re * scale, xn[j].im * scale);
+                psi[j] = C(acc[j].re * (RT)scale, acc[j].im * (RT)scale);
+                xp[j] = C(xn[j].re * (RT)scale, xn[j].im * (RT)scale);
             }
-            xbar = a.w * (s[1] * scale) * scale;
+            xbar = (RT)(a.w * (s[1] * scale) * scale);
             // check_boundary_error: sqrt(sum |psi|^2) > thr, compared squared (no square roots)
             const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
             bool f = stop * sc2 > thr2;
@@ -1177,7 +1241,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R> / 4), (kStepWaves<FAM, R>
 }
 
 // ---- standalone observation / aux / reset kernels --------------------------------------------
-template <int FAM, int R>
+// psi is stored at the handle's precision RT; these kernels compute in fp64 (they run once per
+// control step or per episode).
+template <typename RT>
+__device__ __forceinline__ cd ld_psi(const void* p, size_t i) {
+    const RT* q = (const RT*)p;
+    return C((double)q[2 * i], (double)q[2 * i + 1]);
+}
+template <int FAM, int R, typename RT = double>
 __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1185,10 +1256,10 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
     const int base = lane * R;
     Coef<FAM, R> cf;
     load_coef<FAM, R>(cf, a, base);
-    const double* gpsi = a.psi + (size_t)env * a.N * 2;
+    const size_t e0 = (size_t)env * a.N;
     cd psi[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) psi[j] = (base + j < a.N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < a.N) ? ld_psi<RT>(a.psi, e0 + base + j) : C(0.0, 0.0);
     if constexpr (FAM <= 1) {
         double o[5];
         fock_obs<FAM, R>(psi, cf, lane, o);
@@ -1212,7 +1283,7 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
 
 // what: 0 = x_expectation (double), 1 = outside probability (double), 2 = boundary Fail (int32),
 //       3 = energy Re<psi|H|psi> w at F = 0 (double), 4 = Fock phonon number sum n |psi_n|^2 (double)
-template <int FAM, int R>
+template <int FAM, int R, typename RT = double>
 __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth, void* out) {
     const int lane = threadIdx.x & 63;
     const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1220,10 +1291,10 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
     const int base = lane * R, N = a.N;
     Coef<FAM, R> cf;
     load_coef<FAM, R>(cf, a, base);
-    const double* gpsi = a.psi + (size_t)env * N * 2;
+    const size_t e0 = (size_t)env * N;
     cd psi[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(0.0, 0.0);
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld_psi<RT>(a.psi, e0 + base + j) : C(0.0, 0.0);
     double s[3] = {0.0, 0.0, 0.0};
     if (what == 0) {
         cd xp[R];
@@ -1267,7 +1338,7 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
     }
 }
 
-template <int FAM, int R>
+template <int FAM, int R, typename RT = double>
 __global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const uint8_t* mask, double a0, double a1,
                                                 double a2, const double* k_arr, const double* m_arr,
                                                 const double* s_arr) {
@@ -1276,7 +1347,7 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const ui
     if (env >= a.B) return;
     if (mask && !mask[env]) return;
     const int base = lane * R, N = a.N;
-    double* gpsi = a.psi + (size_t)env * N * 2;
+    RT* gpsi = (RT*)a.psi + (size_t)env * N * 2;
     cd v[R];
     if (kind == 0) {
 #pragma unroll
@@ -1317,8 +1388,8 @@ __global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const ui
 #pragma unroll
     for (int j = 0; j < R; ++j)
         if (base + j < N) {
-            gpsi[2 * (base + j)] = v[j].re;
-            gpsi[2 * (base + j) + 1] = v[j].im;
+            gpsi[2 * (base + j)] = (RT)v[j].re;
+            gpsi[2 * (base + j) + 1] = (RT)v[j].im;
         }
 }
 
@@ -1328,39 +1399,39 @@ namespace qcart {
 
 static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
-template <int FAM, int R, int MODE>
+template <int FAM, int R, int MODE, typename RT>
 int launch_step_mode(const KArgs& a, hipStream_t st) {
-    const dim3 grid(a.n_blocks), block(64 * kStepWaves<FAM, R>);
+    const dim3 grid(a.n_blocks), block(64 * kStepWaves<FAM, R, RT>);
     if (MODE >= 1) {
         static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
         if (!attr_set) {
-            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE, RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024) != hipSuccess)
                 return -3;
             attr_set = true;
         }
     }
-    hipLaunchKernelGGL((k_step<FAM, R, MODE>), grid, block, MODE >= 1 ? a.lds_bytes : 0, st, a);
+    hipLaunchKernelGGL((k_step<FAM, R, MODE, RT>), grid, block, MODE >= 1 ? a.lds_bytes : 0, st, a);
     return 0;
 }
 
-// per-family launch entry points, instantiated in qcart_k_{ho,iho,grid}.hip
-template <int FAM, int R>
+// per-family launch entry points, instantiated in qcart_k_{ho,iho,grid,f32}.hip
+template <int FAM, int R, typename RT = double>
 int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
                double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                void* stream) {
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 4) return kStepWaves<FAM, R>;   // query: envs per step workgroup
+    if (kind == 4) return kStepWaves<FAM, R, RT>;   // query: envs per step workgroup
     if (kind == 0) {
-        const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2>(a, st)
-                     : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1>(a, st)
-                                       : launch_step_mode<FAM, R, 0>(a, st);
+        const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT>(a, st)
+                     : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT>(a, st)
+                                       : launch_step_mode<FAM, R, 0, RT>(a, st);
         if (rc) return rc;
     }
-    else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R>), grid, block, 0, st, a);
-    else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R>), grid, block, 0, st, a, what, xth, out);
-    else hipLaunchKernelGGL((k_reset<FAM, R>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);
+    else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);
+    else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R, RT>), grid, block, 0, st, a, what, xth, out);
+    else hipLaunchKernelGGL((k_reset<FAM, R, RT>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1374,5 +1445,9 @@ int launch_fam1(int R, int kind, const KArgs& a, int what, double xth, void* out
 int launch_fam2(int R, int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
                 double a0, double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                 void* stream);
+// fp32 working precision (C5), Fock families: family 0 / 1
+int launch_f32(int family, int R, int kind, const KArgs& a, int what, double xth, void* out, int rkind,
+               const uint8_t* mask, double a0, double a1, double a2, const double* k_arr, const double* m_arr,
+               const double* s_arr, void* stream);
 
 }  // namespace qcart

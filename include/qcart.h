@@ -54,6 +54,9 @@ enum qc_status {
 
 /* Runtime replacement of setupC.py's compile-time macros (HO/setupC.py:49, QO/setupC.py:55)
  * plus the per-call step() arguments dt / gamma that are fixed for a batch. */
+/* working precision of the step (psi storage and arithmetic) */
+enum qc_precision { QC_FP64 = 0, QC_FP32 = 1 };
+
 typedef struct qc_params {
     int32_t family;        /* enum qc_family                                                     */
     int32_t n_max;         /* Fock: N = n_max + 1  (N_MAX macro)                                 */
@@ -68,7 +71,8 @@ typedef struct qc_params {
     double dt;             /* time step (step() argument; 1/time_steps)                         */
     double f_max;          /* action -> force map F = (a - 10) * f_max / 10 (IHO/RL.py:107-111)  */
     int32_t n_actions;     /* 21 (2*10 + 1, IHO/RL.py:81,94)                                     */
-    int32_t reserved0;
+    int32_t precision;     /* enum qc_precision: 0 fp64 (default, the reference's), 1 fp32 (config C5;
+                              Fock families; psi buffers are then complex64)                     */
     int64_t batch;         /* B envs held by this handle (this rank's shard)                   */
     int64_t env_offset;    /* global id of env 0 (multi-GPU sharding keeps noise invariant)    */
     uint64_t seed;         /* Philox key (replaces set_seed's MT19937 stream, IHO:574-579)     */

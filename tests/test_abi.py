@@ -42,3 +42,27 @@ def test_create_without_gpu_fails_loudly():
     rc = _lib.lib().qc_create(ctypes.byref(p), 0, ctypes.byref(h))
     assert rc < 0 and not h.value
     assert b"HIP" in _lib.lib().qc_last_error(None) or rc == -3
+
+
+def test_params_struct_matches_header(tmp_path):
+    """_lib.QcParams mirrors qc_params exactly: same field order, and (compiled against the header)
+    the same offsets and total size, including the precision field."""
+    import shutil
+    import subprocess
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib
+    txt = open(os.path.join(ROOT, "include", "qcart.h")).read()
+    body = re.search(r"typedef struct qc_params \{(.*?)\} qc_params;", txt, re.S).group(1)
+    names = re.findall(r"^\s*(?:u?int(?:32|64)_t|double)\s+(\w+);", body, re.M)
+    assert names == [f[0] for f in _lib.QcParams._fields_]
+    assert "QC_FP32 = 1" in txt
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    src = tmp_path / "off.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "qcart.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(qc_params, {n}));\n' for n in names)
+                   + 'printf("%zu\\n", sizeof(qc_params));return 0;}\n')
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [getattr(_lib.QcParams, n).offset for n in names] + [ctypes.sizeof(_lib.QcParams)]
+    assert got == want

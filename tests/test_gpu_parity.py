@@ -381,3 +381,64 @@ def test_config_size_batch_properties(oracle_mod, config):
                        n_threads=1)
         err = wnorm(ph, psi[e].cpu().numpy() - ref[0])
         assert err < 1e-10, (e, err)
+
+
+@pytest.mark.parametrize("n_max", [511, 2047])
+def test_fp32_path_tracks_fp64_oracle(oracle_mod, n_max):
+    """fp32 working precision (config C5: IHO N = 2048 in fp32): the complex64 state stays within
+    fp32 accumulation error of the fp64 oracle on identical injected noise (measured ~8e-7 at 200
+    steps; bound 2e-5), and the Fail flag agrees."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max, precision=1, gamma=0.5 * pi)
+    B = 4
+    osys = oracle_sys(oracle_mod, ph)
+    ref = np.zeros((B, ph.dim), np.complex128)
+    ref[:, 0] = 1.0
+    st = Stepper(ph, B, 0, seed=1)
+    psi = torch.from_numpy(ref.astype(np.complex64)).cuda()
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        acts = rng.integers(8, 13, B).astype(np.int32)
+        nz = rng.standard_normal((40, B, 2))
+        f_ref, _, _ = osys.run_batch(ref, acts, ph.f_max, 40, ph.dt, ph.gamma, noise=nz, n_threads=4)
+        out = st.step(psi, torch.from_numpy(acts).cuda(), 40, noise=torch.from_numpy(nz).cuda(), want_fail=True)
+        assert np.array_equal(out["fail_step"].cpu().numpy(), f_ref)
+    err = np.linalg.norm(psi.cpu().numpy().astype(np.complex128) - ref, axis=1)
+    assert err.max() < 2e-5, err
+
+
+def test_fp32_c5_batch_properties(oracle_mod):
+    """C5's per-GPU batch (262144 / 8 envs at N = 2048, fp32): normalised, deterministic, and a sampled
+    env matches the fp64 oracle run alone with the same Philox stream to fp32 accuracy."""
+    conf = cfg.BENCH_CONFIGS["C5"]
+    ph = conf["physics"]
+    B = conf["batch"] // 8
+    st = Stepper(ph, B, 0, seed=7)
+    psi = st.new_state()
+    assert psi.dtype == torch.complex64
+    st.reset(psi, 1, arg0=16)
+    psi0 = psi.clone()
+    acts = torch.randint(0, 21, (B,), generator=torch.Generator(device="cuda").manual_seed(2), device="cuda",
+                         dtype=torch.int32)
+    st.step(psi, acts, 80)
+    st.step_counter = 0
+    again = psi0.clone()
+    st.step(again, acts, 80)
+    torch.cuda.synchronize()
+    assert torch.equal(psi, again)
+    norms = (psi.abs().double() ** 2).sum(1)
+    assert float((norms - 1).abs().max()) < 1e-5
+    osys = oracle_sys(oracle_mod, ph)
+    for e in (0, B - 1):
+        ref = psi0[e:e + 1].cpu().numpy().astype(np.complex128)
+        osys.run_batch(ref, acts[e:e + 1].cpu().numpy(), ph.f_max, 80, ph.dt, ph.gamma, seed=7, env_offset=e,
+                       n_threads=1)
+        err = np.linalg.norm(psi[e].cpu().numpy().astype(np.complex128) - ref[0])
+        assert err < 1e-5, (e, err)
+
+
+def test_fp32_rejects_grid_and_wrong_dtype():
+    with pytest.raises(Exception):
+        Stepper(cfg.DEFAULTS[cfg.IQO].with_(x_max=12.8, precision=1), 2, 0)
+    st = Stepper(cfg.DEFAULTS[cfg.IHO].with_(n_max=511, precision=1), 2, 0)
+    with pytest.raises(ValueError, match="Complex64"):
+        st.step(torch.zeros((2, 512), dtype=torch.complex128, device="cuda"), None, 1)

@@ -14,7 +14,7 @@ echo "kernel-trace rc=$rc"; tail -2 "$ROOT/gpurun_out/prof_kt_$TAG.log"
 [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "$ROOT/gpurun_out/prof_pmc_${C}_$TAG" -o run \
-      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$ROOT/gpurun_out/prof_pmc_${C}_$TAG.log" 2>&1; rc=$?
+      -- python3 "$ROOT/bench.py" $BENCH_ARGS --steps 2 --warmup 1 > "$ROOT/gpurun_out/prof_pmc_${C}_$TAG.log" 2>&1; rc=$?
   echo "pmc $C rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done

@@ -45,12 +45,25 @@ template <typename RT>
 __device__ __forceinline__ cx<RT> cmac(cx<RT> acc, cx<RT> a, cx<RT> b) {   // acc + a*b
     return C(acc.re + a.re * b.re - a.im * b.im, acc.im + a.re * b.im + a.im * b.re);
 }
+// acc - a*b as two FMA chains (4 FP ops; acc - (a*b) as written would cost 6: contraction cannot
+// reassociate the inner difference)
 template <typename RT>
-__device__ __forceinline__ cx<RT> cmsub(cx<RT> acc, cx<RT> a, cx<RT> b) {  // acc - a*b
-    return C(acc.re - (a.re * b.re - a.im * b.im), acc.im - (a.re * b.im + a.im * b.re));
+__device__ __forceinline__ cx<RT> cmsub(cx<RT> acc, cx<RT> a, cx<RT> b) {
+    return C(acc.re + a.im * b.im - a.re * b.re, acc.im - a.im * b.re - a.re * b.im);
 }
 template <typename RT>
 __device__ __forceinline__ cx<RT> ld(const RT* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
+// s + Re<a, b> for one row of a lane-partial sum: fp64 as one FMA chain (the first row starts the
+// chain: no "+ 0"), fp32 products summed in fp32 and accumulated in fp64
+template <typename RT>
+__device__ __forceinline__ double dot_acc(double s, bool first, cx<RT> a, cx<RT> b) {
+    if constexpr (sizeof(RT) == 8) {
+        return first ? a.re * b.re + a.im * b.im : s + a.re * b.re + a.im * b.im;
+    } else {
+        const double p = (double)(a.re * b.re + a.im * b.im);
+        return first ? p : s + p;
+    }
+}
 // Factor-block reads: one buffer descriptor per slot block (SGPRs), per-lane VGPR offset, constant
 // SGPR / immediate byte offsets. Out-of-range reads return 0 (descriptor bounds = block size).
 using rsrc_t = __amdgpu_buffer_rsrc_t;
@@ -650,7 +663,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     for (int j = 0; j < R; ++j) {
         cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
+        for (int k = KL - 1; k >= 0; --k)   // s[k] = y_{j-1-k}: zero for k >= j (no multiplies by 0)
+            if (k < j) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
@@ -699,7 +713,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
         b[j] = cmul(tb.c(SL.di + (uint32_t)j * CE), b[j]);   // D^-1 y, reused by pass 2
         cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
+        for (int k = KL - 1; k >= 0; --k)   // s[k] = x_{j+1+k}: zero for j + k >= R - 1
+            if (j + k < R - 1) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -947,7 +962,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
     const double inv_sdt = 1.0 / sdt, inv_dt = 1.0 / dt;
     // vector-facing constants at the working precision
-    const RT g4r = (RT)g4, dtr = (RT)dt, a2r = (RT)a.a2, a3r = (RT)a.a3, a4r = (RT)a.a4, a5r = (RT)a.a5;
+    const RT g4r = (RT)g4, dtr = (RT)dt, a5r = (RT)a.a5;
+    const RT b2r = (RT)(a.a2 / a.a5), b3r = (RT)(a.a3 / a.a5), b4r = (RT)(a.a4 / a.a5);   // term7 Horner / a5
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
@@ -1016,30 +1032,29 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         }
         QC_STAMP(1);
         {
-            // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3)
+            // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3), Horner in H_F on A/a5
+            // (coefficients a_k/a5; a5 applied once in the sum below: no separate i a5 D1 pass)
             auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
                 if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lane);
                 else apply_hf<FAM, R>(v, u, cF, cf, lane);
             };
             cx<RT> t[R];
+            hf(D1, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(-a5r * D1[j].im, a5r * D1[j].re);
+            for (int j = 0; j < R; ++j) t[j] = C(-acc[j].im - b4r * D1[j].re, acc[j].re - b4r * D1[j].im);
             hf(t, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re - a4r * D1[j].re, acc[j].im - a4r * D1[j].im);
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b3r * D1[j].im, acc[j].im - b3r * D1[j].re);
             hf(t, acc);
 #pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a3r * D1[j].im, acc[j].im - a3r * D1[j].re);
-            hf(t, acc);
-#pragma unroll
-            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + a2r * D1[j].re, acc[j].im + a2r * D1[j].im);
+            for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b2r * D1[j].re, acc[j].im + b2r * D1[j].im);
             hf(t, acc);
             hf(acc, t);
             const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2);
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re + t[j].re,
-                           psi[j].im + kA * rel[j].im + k2 * D1[j].im + t[j].im);
+                acc[j] = C(psi[j].re + kA * rel[j].re + k2 * D1[j].re + a5r * t[j].re,
+                           psi[j].im + kA * rel[j].im + k2 * D1[j].im + a5r * t[j].im);
                 psi[j] = C(psi[j].re + dtr * D1[j].re, psi[j].im + dtr * D1[j].im);   // Y0
             }
         }
@@ -1089,8 +1104,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             double sm[2] = {0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                sm[0] += (double)(psi[j].re * xYp[j].re + psi[j].im * xYp[j].im);
-                sm[1] += (double)(Ym[j].re * xYm[j].re + Ym[j].im * xYm[j].im);
+                sm[0] = dot_acc(sm[0], j == 0, psi[j], xYp[j]);
+                sm[1] = dot_acc(sm[1], j == 0, Ym[j], xYm[j]);
             }
             wave_sum<2>(sm);
             yp = a.w * sm[0];
@@ -1125,24 +1140,23 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 rp[j] = C(xYp[j].re - ypr * psi[j].re, xYp[j].im - ypr * psi[j].im);   // rel+
             });
             apply_x<FAM, R>(rp, xrp, cf, lane);
-            const double kRed = -(c1 + c2) * g4;
-            const RT kRe = (RT)kRed, kDp = (RT)((c3 + c4 - c5) * beta - kRed * yp);
+            const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp;
             QC_STAMP(5);
             // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
             //   pp/pm = yp +- w kP (<Y+, X rel+> + <rel+, X Y+>) + w kP^2 <rel+, X rel+>
             double d2[2] = {0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                acc[j] = C(acc[j].re + kRe * xrp[j].re + kDp * rp[j].re, acc[j].im + kRe * xrp[j].im + kDp * rp[j].im);
-                d2[0] += (double)(psi[j].re * xrp[j].re + psi[j].im * xrp[j].im + rp[j].re * xYp[j].re + rp[j].im * xYp[j].im);
-                d2[1] += (double)(rp[j].re * xrp[j].re + rp[j].im * xrp[j].im);
+                d2[0] = dot_acc(dot_acc(d2[0], j == 0, psi[j], xrp[j]), false, rp[j], xYp[j]);
+                d2[1] = dot_acc(d2[1], j == 0, rp[j], xrp[j]);
             }
             wave_sum<2>(d2);
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
             const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
-            const RT fx = (RT)(2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(-k5 * kP * spm);
+            // with this branch's kRe X rel+ + kDp rel+ folded in (one pass over acc)
+            const RT fx = (RT)(kRed + 2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(kDpd - k5 * kP * spm);
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 acc[j] = C(acc[j].re + fx * xrp[j].re + fy * psi[j].re + fr * rp[j].re,
@@ -1158,24 +1172,37 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             apply_x<FAM, R>(acc, xn, cf, lane);
             // full reductions only for the norm and the next <x>; the boundary sums (Fail) touch the
             // few lanes holding the edge rows and are read from them directly
-            double s[2] = {0.0, 0.0}, ptop = 0.0, pbot = 0.0, pwin = 0.0;
+            double s[2] = {0.0, 0.0}, pwin = 0.0, stop = 0.0, sbot = 0.0;
+            if constexpr (FAM <= 1) {
+                // rows high -> low as FMA chains; the boundary band [N - bnd_len, N) starts at row jt of
+                // lane lt: that lane's suffix sum from jt is captured on the way, the lanes above add
+                // whole (rows >= N are zero padding)
+                const int r0 = N - a.bnd_len, lt = r0 / R, jt = r0 - lt * R;
+                double suf = 0.0;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
-                s[0] += p2;
-                s[1] += (double)(acc[j].re * xn[j].re + acc[j].im * xn[j].im);
-                const int r = base + j;
-                if (r >= N - a.bnd_len && r < N) ptop += p2;
-                if constexpr (FAM == 2) {
+                for (int j = R - 1; j >= 0; --j) {
+                    s[0] = dot_acc(s[0], j == R - 1, acc[j], acc[j]);
+                    s[1] = dot_acc(s[1], j == R - 1, acc[j], xn[j]);
+                    if (j == jt) suf = s[0];
+                }
+                stop = readlane_d(suf, lt);
+                for (int l = lt + 1; l <= (N - 1) / R; ++l) stop += readlane_d(s[0], l);
+            } else {
+                double ptop = 0.0, pbot = 0.0;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
+                    s[0] += p2;
+                    s[1] += (double)(acc[j].re * xn[j].re + acc[j].im * xn[j].im);
+                    const int r = base + j;
+                    if (r >= N - a.bnd_len && r < N) ptop += p2;
                     if (r < a.bnd_len) pbot += p2;
                     if (r >= a.win_lo && r < a.win_hi) pwin += p2;
                 }
+                for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
+                for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
             }
             wave_sum<2>(s);
-            double stop = 0.0, sbot = 0.0;
-            for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
-            if constexpr (FAM == 2)
-                for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
             // 1/sqrt(s0): hardware estimate + two Newton steps (full fp64 precision)
             double scale = __builtin_amdgcn_rsq(s[0]);
             scale = scale * (1.5 - 0.5 * s[0] * scale * scale);

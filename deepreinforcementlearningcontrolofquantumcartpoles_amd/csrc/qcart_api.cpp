@@ -208,10 +208,11 @@ KArgs base_args(const qc_handle* h) {
         const bool f32 = p.precision == QC_FP32;
         const uint32_t es = f32 ? 8u : 16u;   // bytes per complex table element
         const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO, es);
-        const size_t t1 = L.tf, t2 = L.tf + (size_t)(lf + lb + 2) * op.kl * op.kl * kWave * es;
+        // MODE 2 image: levels 0..3 + the row prefix per direction at fixed places (needs kf, kb <= 4)
+        const size_t t1 = L.tf, t2 = L.tf + (size_t)10 * op.kl * op.kl * kWave * es;
         // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
         const size_t fx = (op.fock && !f32) ? (size_t)(op.R + 1) * kWave * 8 : 0;
-        int mode = t2 + fx <= 160 * 1024 ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
+        int mode = (t2 + fx <= 160 * 1024 && lf <= 4 && lb <= 4) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
         a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);

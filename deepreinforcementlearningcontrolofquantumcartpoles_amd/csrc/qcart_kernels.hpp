@@ -181,7 +181,21 @@ __device__ __forceinline__ float add_swap32(float v) {
     const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(a[0]) + __uint_as_float(a[1]);
 }
-// all-lane sum; every pairing is symmetric, so every lane ends with bit-identical values
+// DPP with an explicit row mask; rows not in the mask read 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_dm(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    return mk_d((unsigned)lo, (unsigned)hi);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_dm(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+}
+// all-lane sum: butterflies inside each 16-lane row (every lane ends with its row's sum), then the
+// rows fold up through row_bcast:15 / row_bcast:31 into lane 63, whose value is read as the one
+// (wave-uniform) total
 template <int NV, typename RT>
 __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
 #pragma unroll
@@ -193,9 +207,11 @@ __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x140>(v[i]);   // row_mirror
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = add_swap16(v[i]);
+    for (int i = 0; i < NV; ++i) v[i] += dpp_dm<0x142, 0xa>(v[i]);   // rows 1, 3 += rows 0, 2
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = add_swap32(v[i]);
+    for (int i = 0; i < NV; ++i) v[i] += dpp_dm<0x143, 0xc>(v[i]);   // rows 2, 3 += rows 0 + 1
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = readlane_d(v[i], 63);
 }
 
 // ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
@@ -559,23 +575,11 @@ struct Tab {
         else return bld_d<RT>(rs, vr, (int)off);
     }
     __device__ __forceinline__ cx<RT> comp(uint32_t off) const {   // scan composites
-        if constexpr (MODE == 2) return lds_c(lds + vc + off);
+        if constexpr (MODE == 2) return lds_c(atc(off));
         else return bld_c<RT>(rs, vc, (int)off);
     }
 };
 
-// DPP with an explicit row mask; rows not in the mask keep 0
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_dm(double v) {
-    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), CTRL, ROWMASK, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
-    return mk_d((unsigned)lo, (unsigned)hi);
-}
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_dm(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, false));
-}
 // in-row shifts (16-lane DPP rows; sources outside the row read 0)
 template <int D, bool UP, typename RT>
 __device__ __forceinline__ cx<RT> row_shift(cx<RT> v) {
@@ -651,10 +655,12 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
     constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>));
     constexpr uint32_t CB = KL * KL * CE;
-    const uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + (uint32_t)kf * CB : SL.tf + 6u * CB;
-    const uint32_t b0 = MODE == 2 ? SL.tf + (uint32_t)(kf + 1) * CB : SL.tb;
-    const uint32_t bP = MODE == 2 ? SL.tf + (uint32_t)(kf + 1 + kb) * CB : SL.tb + 6u * CB;
-    const bool hf = kf <= 4, hb = kb <= 4;
+    // MODE 2 image (fixed, compile-time offsets): forward levels 0..3, forward P, backward 0..3, backward P
+    // (the host uses MODE 2 only when every slot keeps <= 4 levels per direction)
+    constexpr uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + 4u * CB : SL.tf + 6u * CB;
+    constexpr uint32_t b0 = MODE == 2 ? SL.tf + 5u * CB : SL.tb;
+    constexpr uint32_t bP = MODE == 2 ? SL.tf + 9u * CB : SL.tb + 6u * CB;
+    const bool hf = MODE == 2 || kf <= 4, hb = MODE == 2 || kb <= 4;
     // forward, pass 1 (zero incoming state): lane end state e_l
     cx<RT> s[KL];
 #pragma unroll
@@ -912,12 +918,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             }
         };
         copy(0, 0, SL.tf);
-        if constexpr (MODE == 2) {
+        if constexpr (MODE == 2) {   // the kept composite levels at their fixed places (band_solve)
             constexpr uint32_t CB = KL * KL * CE;
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
-            copy(SL.tf + 6u * CB, SL.tf + (uint32_t)kf * CB, CB);
-            copy(SL.tb, SL.tf + (uint32_t)(kf + 1) * CB, (uint32_t)kb * CB);
-            copy(SL.tb + 6u * CB, SL.tf + (uint32_t)(kf + 1 + kb) * CB, CB);
+            copy(SL.tf + 6u * CB, SL.tf + 4u * CB, CB);
+            copy(SL.tb, SL.tf + 5u * CB, (uint32_t)kb * CB);
+            copy(SL.tb + 6u * CB, SL.tf + 9u * CB, CB);
         }
         if constexpr (FXL) {
             if (threadIdx.x < 64) {

@@ -16,6 +16,7 @@ CASES = [
     ("QO N=171", cfg.DEFAULTS[cfg.QO], 65536),
     ("QO N=1024 (C3)", cfg.BENCH_CONFIGS["C3"]["physics"], 16384),
     ("IQO N=513 (C4)", cfg.BENCH_CONFIGS["C4"]["physics"], 65536),
+    ("IHO N=2048 fp32 (C5)", cfg.BENCH_CONFIGS["C5"]["physics"], 32768),
 ]
 
 
@@ -38,7 +39,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 3
-        print(f"{name:16s} N={ph.dim:5d} B={B:6d}  {ms:8.2f} ms / {n} steps  {B * n / ms * 1e3:.4g} env-steps/s"
+        print(f"{name:20s} N={ph.dim:5d} B={B:6d}  {ms:8.2f} ms / {n} steps  {B * n / ms * 1e3:.4g} env-steps/s"
               f"  {B * n * ph.dim / ms * 1e3:.4g} row-steps/s", flush=True)
 
 

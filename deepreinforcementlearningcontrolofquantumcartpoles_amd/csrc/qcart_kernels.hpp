@@ -195,7 +195,8 @@ __device__ __forceinline__ float dpp_dm(float v) {
 }
 // all-lane sum: butterflies inside each 16-lane row (every lane ends with its row's sum), then the
 // rows fold up through row_bcast:15 / row_bcast:31 into lane 63, whose value is read as the one
-// (wave-uniform) total
+// (wave-uniform) total. Only lane 63's chain matters, so the broadcasts need no row mask (and no
+// zeroed destination)
 template <int NV, typename RT>
 __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
 #pragma unroll
@@ -207,9 +208,9 @@ __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x140>(v[i]);   // row_mirror
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] += dpp_dm<0x142, 0xa>(v[i]);   // rows 1, 3 += rows 0, 2
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x142>(v[i]);   // row k += row k-1 (row_bcast:15)
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] += dpp_dm<0x143, 0xc>(v[i]);   // rows 2, 3 += rows 0 + 1
+    for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x143>(v[i]);   // rows 2, 3 += lane 31 (row_bcast:31)
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = readlane_d(v[i], 63);
 }
@@ -631,7 +632,7 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
         } else {
             // first lane of row r+1 -> lane 15 of row r (wave_shl:1) -> every lane of row r
             const cx<RT> t = C(shl1(s[k].re), shl1(s[k].im));
-            c[k] = C(dpp_dm<0x15F, 0xf>(t.re), dpp_dm<0x15F, 0xf>(t.im));
+            c[k] = C(dpp_d<0x15F>(t.re), dpp_d<0x15F>(t.im));   // row_newbcast:15 (every row, all lanes)
         }
     }
 #pragma unroll

@@ -27,6 +27,8 @@ EXPORTS = (
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
     "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_scan_levels",
+    "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
+    "qc_actor_noise_len", "qc_actor_act",
 )
 
 
@@ -50,6 +52,25 @@ class QcParams(ctypes.Structure):
         ("env_offset", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
         ("xth", ctypes.c_double),
+    ]
+
+
+class QcDqnParams(ctypes.Structure):
+    _fields_ = [
+        ("data_length", ctypes.c_int32),
+        ("n_actions", ctypes.c_int32),
+        ("max_batch", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class QcDqnLayer(ctypes.Structure):
+    _fields_ = [
+        ("weight", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p),
+        ("weight_norm", ctypes.c_void_p),
+        ("sigma_w", ctypes.c_void_p),
+        ("sigma_b", ctypes.c_void_p),
     ]
 
 
@@ -108,12 +129,28 @@ def lib() -> ctypes.CDLL:
     L.qc_phonon_number.argtypes = [vp, vp, vp]
     L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
+    L.qc_actor_create.argtypes = [P(QcDqnParams), ctypes.c_int, P(vp)]
+    L.qc_actor_destroy.argtypes = [vp]
+    L.qc_actor_destroy.restype = None
+    L.qc_actor_last_error.argtypes = [vp]
+    L.qc_actor_last_error.restype = ctypes.c_char_p
+    L.qc_actor_set_stream.argtypes = [vp, vp]
+    L.qc_actor_load.argtypes = [vp, P(QcDqnLayer)]
+    L.qc_actor_noise_len.argtypes = [vp]
+    L.qc_actor_act.argtypes = [vp, i64, i64, vp, i32, vp, d, u64, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int:   # default
             fn.restype = ctypes.c_int
     _lib = L
     return L
+
+
+def check_actor(rc: int, handle=None) -> int:
+    if rc < 0:
+        msg = lib().qc_actor_last_error(handle)
+        raise QCartError(rc, msg.decode() if msg else "")
+    return rc
 
 
 def check(rc: int, handle=None) -> int:

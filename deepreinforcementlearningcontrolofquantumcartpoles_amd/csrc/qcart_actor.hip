@@ -1,0 +1,453 @@
+// qcart_actor.hip — batched DQN actor: the reference's direct_DQN action selection
+// for B envs per launch, fused fc1 -> fc2 -> fc31 -> fc41 -> argmax -> epsilon-greedy.
+//
+// Reference: inverted harmonic oscillator/RL.py:80-111 (direct_DQN), layers.py:7-79 (FactorizedNoisy),
+// layers.py:97-103 (Linear_weight_normalize), main_parallel.py:208-219 (epsilon-greedy in the actor) and
+// :414-440 (the inference process: argmax of the action values).
+//
+// Design (MI355X): one workgroup = 32 envs x 4 waves. Every layer is Y[o][env] = W[o][k] X[k][env] on
+// the f32-input MFMA v_mfma_f32_32x32x2_f32 (exact f32 accumulation): A = the layer's weights, stored
+// once per load in fragment order (one coalesced 256-B read per MFMA), B = the activations in LDS as
+// [feature][32 envs] (one conflict-free ds_read_b32 per MFMA), D = a 32-feature x 32-env tile whose
+// rows land in the 16 accumulator registers. The epilogue adds bias / noise, applies ReLU and writes
+// the next layer's input back to LDS; activations never leave the CU. A factorised noisy layer is two
+// GEMMs per tile: u_w X and sigma_w (eps_in o X), combined as
+//   y = u_w x + u_b + eps_out o (sigma_w (eps_in o x) + sigma_b)   (== (u_w + sigma_w o eps_out eps_in^T) x + ...)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <mutex>
+#include <string>
+
+#include "../../include/qcart.h"
+#include "qcart_kernels.hpp"
+
+namespace qcart {
+namespace actor {
+
+constexpr int kE = 32;                 // envs per workgroup (one MFMA column block)
+constexpr int kH1 = 512, kH2 = 256, kH3 = 256;
+constexpr int kMaxIn = 512;            // data_length limit (LDS: [in][32] fp32 within 64 KiB)
+constexpr int kThreads = 256;
+using f32x16 = float __attribute__((ext_vector_type(16)));
+
+// fragment buffer of one [O][K] matrix: tiles of 32 outputs x K/2 steps x 64 lanes
+__host__ __device__ constexpr int tiles(int O) { return (O + 31) / 32; }
+__host__ __device__ constexpr int ksteps(int K) { return (K + 1) / 2; }
+
+struct Layer {
+    const float* u;      // fragments of the (effective) weight
+    const float* s;      // fragments of sigma_w (noisy) or null
+    const float* ub;     // bias, padded to tiles*32
+    const float* sb;     // sigma_b, padded, or null
+};
+
+struct ActArgs {
+    Layer L[4];
+    int in_len, in_pad, n_act;
+    int64_t B, env_offset;
+    const float* obs;
+    int noisy;
+    const float* noise;   // [noise_len][B] feature-major (internal layout)
+    int64_t noise_ld;     // leading dimension of the noise buffer (>= B)
+    float eps;
+    uint64_t seed, counter;
+    int32_t* actions;
+    float* q_out;
+    int32_t* random_out;
+};
+
+// acc += A_frag(W) . X  over `steps` k-steps (X: LDS [k][32]; lane reads X[2s + (lane>>5)][lane&31])
+__device__ __forceinline__ void gemm_tile(f32x16& acc, const float* __restrict__ wf, const float* x, int steps,
+                                          int lane) {
+    const float* xl = x + (lane >> 5) * kE + (lane & 31);
+    const float* wl = wf + lane;
+    int s = 0;
+    for (; s + 8 <= steps; s += 8) {
+        float a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = wl[(s + u) * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = xl[(s + u) * 2 * kE];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+    }
+    for (; s < steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[s * 64], xl[s * 2 * kE], acc, 0, 0, 0);
+}
+
+// D-tile element r of this lane: output row (within the tile) and env column
+__device__ __forceinline__ int drow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ float noise_at(const ActArgs& a, int f, int64_t e) {
+    return a.noise[(int64_t)f * a.noise_ld + e];
+}
+
+__global__ __launch_bounds__(kThreads) void k_actor_act(const ActArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* RA = lds;                      // H1 [512][32]; later H3 [256][32] + H3e [256][32]
+    float* RB = lds + kH1 * kE;           // X0 [in_pad][32]; later H2 [256][32] + H2e [256][32]
+    float* RC = lds + 2 * kH1 * kE;       // fc41 sigma partial [32 rows][64 lanes... as D regs]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t e0 = (int64_t)blockIdx.x * kE;
+    const int env = lane & 31;
+    const int64_t eg = e0 + env;          // this lane's env (D column)
+    const bool env_ok = eg < a.B;
+
+    // ---- input: the fp32 network input (IHO/main_parallel.py:131,241) -> X0[k][env]
+    for (int i = tid; i < a.in_pad * kE; i += kThreads) {
+        const int k = i / kE, e = i % kE;
+        RB[i] = (k < a.in_len && e0 + e < a.B) ? a.obs[(e0 + e) * a.in_len + k] : 0.f;
+    }
+    __syncthreads();
+
+    // ---- fc1: 512 outputs = 16 tiles, 4 per wave; ReLU
+    for (int t = wave; t < tiles(kH1); t += 4) {
+        f32x16 acc = {};
+        gemm_tile(acc, a.L[0].u + (size_t)t * ksteps(a.in_pad) * 64, RB, ksteps(a.in_pad), lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = t * 32 + drow(r, lane);
+            RA[o * kE + env] = fmaxf(acc[r] + a.L[0].ub[o], 0.f);
+        }
+    }
+    __syncthreads();
+
+    // ---- fc2: 256 outputs = 8 tiles, 2 per wave; ReLU; also eps_in(fc31) o H2 for the noisy GEMM
+    float* H2 = RB;
+    float* H2e = RB + kH2 * kE;
+    const bool n31 = a.noisy && a.L[2].s != nullptr;
+    for (int t = wave; t < tiles(kH2); t += 4) {
+        f32x16 acc = {};
+        gemm_tile(acc, a.L[1].u + (size_t)t * ksteps(kH1) * 64, RA, ksteps(kH1), lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = t * 32 + drow(r, lane);
+            const float h = fmaxf(acc[r] + a.L[1].ub[o], 0.f);
+            H2[o * kE + env] = h;
+            if (n31) H2e[o * kE + env] = env_ok ? h * noise_at(a, o, eg) : 0.f;
+        }
+    }
+    __syncthreads();
+
+    // ---- fc31 (noisy or weight-normalised): 8 tiles, 2 per wave; ReLU; eps_in(fc41) o H3
+    float* H3 = RA;
+    float* H3e = RA + kH3 * kE;
+    const bool n41 = a.noisy && a.L[3].s != nullptr;
+    for (int t = wave; t < tiles(kH3); t += 4) {
+        f32x16 acc = {}, accs = {};
+        gemm_tile(acc, a.L[2].u + (size_t)t * ksteps(kH2) * 64, H2, ksteps(kH2), lane);
+        if (n31) gemm_tile(accs, a.L[2].s + (size_t)t * ksteps(kH2) * 64, H2e, ksteps(kH2), lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = t * 32 + drow(r, lane);
+            float y = acc[r] + a.L[2].ub[o];
+            if (n31) y += env_ok ? noise_at(a, kH2 + o, eg) * (accs[r] + a.L[2].sb[o]) : 0.f;
+            const float h = fmaxf(y, 0.f);
+            H3[o * kE + env] = h;
+            if (n41) H3e[o * kE + env] = env_ok ? h * noise_at(a, 2 * kH2 + o, eg) : 0.f;
+        }
+    }
+    __syncthreads();
+
+    // ---- fc41: one 32-row tile; wave 0: u_w H3, wave 1: sigma_w (eps_in o H3) -> LDS partial
+    if (wave == 1 && n41) {
+        f32x16 accs = {};
+        gemm_tile(accs, a.L[3].s, H3e, ksteps(kH3), lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) RC[r * 64 + lane] = accs[r];
+    }
+    f32x16 acc = {};
+    if (wave == 0) gemm_tile(acc, a.L[3].u, H3, ksteps(kH3), lane);
+    __syncthreads();
+    if (wave != 0) return;
+
+    // ---- action values, argmax (lowest index among equal maxima), epsilon-greedy
+    float best = -INFINITY;
+    int besti = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int o = drow(r, lane);
+        if (o < a.n_act) {
+            float q = acc[r] + a.L[3].ub[o];
+            if (n41) q += env_ok ? noise_at(a, 2 * kH2 + kH3 + o, eg) * (RC[r * 64 + lane] + a.L[3].sb[o]) : 0.f;
+            if (a.q_out && env_ok) a.q_out[eg * a.n_act + o] = q;
+            if (q > best || (q == best && o < besti)) {
+                best = q;
+                besti = o;
+            }
+        }
+    }
+    const float ob = __shfl_xor(best, 32, 64);
+    const int oi = __shfl_xor(besti, 32, 64);
+    if (ob > best || (ob == best && oi < besti)) besti = oi;
+    if (lane < 32 && env_ok) {
+        int act = besti;
+        int rnd = 0;
+        if (a.eps > 0.f) {
+            uint32_t c[4] = {(uint32_t)a.counter, (uint32_t)(a.counter >> 32), (uint32_t)(a.env_offset + eg), 0x200u};
+            philox10(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+            const float u1 = (float)(c[0] >> 8) * 0x1.0p-24f, u2 = (float)(c[1] >> 8) * 0x1.0p-24f;
+            if (u1 < a.eps) {   // random.random() < eps_threshold -> random.randrange(21)
+                act = min((int)(u2 * (float)a.n_act), a.n_act - 1);
+                rnd = 1;
+            }
+        }
+        a.actions[eg] = act;
+        if (a.random_out) a.random_out[eg] = rnd;
+    }
+}
+
+// NoisyNet noise, feature-major [noise_len][ld]: f(z) = sign(z) sqrt|z| (layers.py:77-79) of Philox
+// normals keyed by (seed, env_offset + e), counter, tag 0x100 + pair
+__global__ __launch_bounds__(256) void k_actor_noise(float* out, int64_t ld, int64_t B, int noise_len,
+                                                     int64_t env_offset, uint64_t seed, uint64_t counter) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int p = blockIdx.y;
+    if (e >= B) return;
+    double z0, z1;
+    normals(seed, (uint32_t)(env_offset + e), counter, 0x100u + (uint32_t)p, z0, z1);
+    const float f0 = (float)z0, f1 = (float)z1;
+    out[(int64_t)(2 * p) * ld + e] = copysignf(sqrtf(fabsf(f0)), f0);
+    if (2 * p + 1 < noise_len) out[(int64_t)(2 * p + 1) * ld + e] = copysignf(sqrtf(fabsf(f1)), f1);
+}
+
+// injected noise [B][noise_len] -> feature-major [noise_len][ld]
+__global__ __launch_bounds__(256) void k_actor_transpose(const float* in, float* out, int64_t ld, int64_t B,
+                                                         int noise_len) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * noise_len) return;
+    const int64_t e = i / noise_len;
+    const int f = (int)(i % noise_len);
+    out[(int64_t)f * ld + e] = in[i];
+}
+
+// effective weight (W g / ||W||_F, or W) -> fragments [tile][step][64]; bias padded to tiles*32
+__global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float* g, int O, int K, int Kpad,
+                                                     float* frag, const float* bias, float* bias_pad) {
+    __shared__ double part[1024];
+    double ss = 0.0;
+    if (g) {
+        for (int i = threadIdx.x; i < O * K; i += 1024) ss += (double)W[i] * (double)W[i];
+    }
+    part[threadIdx.x] = ss;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    const float sc = g ? (float)((double)g[0] / sqrt(part[0])) : 1.f;
+    const int T = tiles(O), S = ksteps(Kpad);
+    for (int i = threadIdx.x; i < T * S * 64; i += 1024) {
+        const int l = i & 63, s = (i >> 6) % S, t = (i >> 6) / S;
+        const int o = t * 32 + (l & 31), k = 2 * s + (l >> 5);
+        frag[i] = (o < O && k < K) ? W[(size_t)o * K + k] * sc : 0.f;
+    }
+    if (bias_pad)
+        for (int i = threadIdx.x; i < T * 32; i += 1024) bias_pad[i] = (i < O && bias) ? bias[i] : 0.f;
+}
+
+}  // namespace actor
+}  // namespace qcart
+
+using namespace qcart::actor;
+
+struct qc_actor {
+    qc_dqn_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int in_pad = 0, noise_len = 0;
+    bool loaded = false;
+    bool has_s[4] = {false, false, false, false};
+    std::string err;
+    float* d_w = nullptr;        // all fragments + padded biases
+    size_t off_u[4]{}, off_s[4]{}, off_ub[4]{}, off_sb[4]{};
+    size_t w_floats = 0;
+    float* d_noise = nullptr;    // [noise_len][max_batch]
+};
+
+namespace {
+std::mutex g_actor_mu;
+std::string g_actor_err;
+
+struct Dev {
+    int prev = -1;
+    explicit Dev(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~Dev() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int hip_fail(qc_actor* a, hipError_t e, const char* what) {
+    a->err = std::string(what) + ": " + hipGetErrorString(e);
+    return QC_EHIP;
+}
+
+constexpr int kLayerO[4] = {kH1, kH2, kH3, 0};
+}  // namespace
+
+extern "C" {
+
+int qc_actor_create(const qc_dqn_params* p, int device, qc_actor** out) {
+    if (!out || !p) return QC_EINVAL;
+    *out = nullptr;
+    auto fail = [](const char* m, int rc) {
+        std::lock_guard<std::mutex> lk(g_actor_mu);
+        g_actor_err = m;
+        return rc;
+    };
+    if (p->data_length < 1 || p->data_length > kMaxIn) return fail("data_length must be in [1, 512]", QC_EINVAL);
+    if (p->n_actions < 1 || p->n_actions > 32) return fail("n_actions must be in [1, 32]", QC_EINVAL);
+    if (p->max_batch < 1) return fail("max_batch must be >= 1", QC_EINVAL);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail("no HIP device available (the actor has no CPU fallback)", QC_EHIP);
+    if (device < 0 || device >= ndev) return fail("device index out of range", QC_EINVAL);
+    qc_actor* a = new qc_actor();
+    a->p = *p;
+    a->device = device;
+    a->in_pad = (p->data_length + 1) & ~1;
+    a->noise_len = 2 * kH2 + kH3 + p->n_actions;
+    const int K[4] = {a->in_pad, kH1, kH2, kH3};
+    const int O[4] = {kH1, kH2, kH3, p->n_actions};
+    size_t off = 0;
+    for (int l = 0; l < 4; ++l) {
+        const size_t fr = (size_t)tiles(O[l]) * ksteps(K[l]) * 64, bp = (size_t)tiles(O[l]) * 32;
+        a->off_u[l] = off; off += fr;
+        a->off_s[l] = off; off += fr;
+        a->off_ub[l] = off; off += bp;
+        a->off_sb[l] = off; off += bp;
+    }
+    a->w_floats = off;
+    Dev g(device);
+    hipError_t e = hipMalloc(&a->d_w, off * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(a->d_w, 0, off * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_noise, (size_t)a->noise_len * (size_t)p->max_batch * sizeof(float));
+    if (e != hipSuccess) {
+        if (a->d_w) (void)hipFree(a->d_w);
+        if (a->d_noise) (void)hipFree(a->d_noise);
+        delete a;
+        return fail("device allocation failed", QC_ENOMEM);
+    }
+    if (hipFuncSetAttribute((const void*)k_actor_act, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (2 * kH1 * kE + 16 * 64) * (int)sizeof(float)) != hipSuccess) {
+        (void)hipFree(a->d_w);
+        (void)hipFree(a->d_noise);
+        delete a;
+        return fail("cannot enable 140 KiB of LDS for the actor kernel", QC_EHIP);
+    }
+    *out = a;
+    (void)kLayerO;
+    return QC_OK;
+}
+
+void qc_actor_destroy(qc_actor* a) {
+    if (!a) return;
+    {
+        Dev g(a->device);
+        (void)hipDeviceSynchronize();
+        if (a->d_w) (void)hipFree(a->d_w);
+        if (a->d_noise) (void)hipFree(a->d_noise);
+    }
+    delete a;
+}
+
+const char* qc_actor_last_error(const qc_actor* a) {
+    if (a) return a->err.c_str();
+    std::lock_guard<std::mutex> lk(g_actor_mu);
+    return g_actor_err.c_str();
+}
+
+int qc_actor_set_stream(qc_actor* a, void* stream) {
+    if (!a) return QC_EINVAL;
+    a->stream = (hipStream_t)stream;
+    return QC_OK;
+}
+
+int qc_actor_noise_len(const qc_actor* a) { return a ? a->noise_len : QC_EINVAL; }
+
+int qc_actor_load(qc_actor* a, const qc_dqn_layer layers[4]) {
+    if (!a || !layers) return QC_EINVAL;
+    const int K[4] = {a->p.data_length, kH1, kH2, kH3};
+    const int Kp[4] = {a->in_pad, kH1, kH2, kH3};
+    const int O[4] = {kH1, kH2, kH3, a->p.n_actions};
+    for (int l = 0; l < 4; ++l) {
+        const qc_dqn_layer& L = layers[l];
+        if (!L.weight || !L.bias) { a->err = "layer " + std::to_string(l) + ": weight and bias are required"; return QC_EINVAL; }
+        if (l < 2 && (!L.weight_norm || L.sigma_w)) {
+            a->err = "fc1 / fc2 are Linear_weight_normalize layers (weight_norm required, no sigma)";
+            return QC_EINVAL;
+        }
+        if ((L.sigma_w == nullptr) != (L.sigma_b == nullptr)) { a->err = "sigma_w and sigma_b go together"; return QC_EINVAL; }
+        if (L.sigma_w && L.weight_norm) { a->err = "a noisy layer has no weight_norm"; return QC_EINVAL; }
+        if (!L.sigma_w && !L.weight_norm) { a->err = "a deterministic layer needs weight_norm"; return QC_EINVAL; }
+    }
+    Dev g(a->device);
+    float* w = a->d_w;
+    for (int l = 0; l < 4; ++l) {
+        const qc_dqn_layer& L = layers[l];
+        hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.weight, L.weight_norm, O[l], K[l], Kp[l],
+                           w + a->off_u[l], L.bias, w + a->off_ub[l]);
+        a->has_s[l] = L.sigma_w != nullptr;
+        if (L.sigma_w)
+            hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.sigma_w, (const float*)nullptr, O[l],
+                               K[l], Kp[l], w + a->off_s[l], L.sigma_b, w + a->off_sb[l]);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(a, e, "actor weight preparation");
+    a->loaded = true;
+    return QC_OK;
+}
+
+int qc_actor_act(qc_actor* a, int64_t B, int64_t env_offset, const float* obs, int32_t noisy, const float* noise,
+                 double eps, uint64_t counter, int32_t* actions, float* q_out, int32_t* random_out) {
+    if (!a) return QC_EINVAL;
+    if (!a->loaded) { a->err = "qc_actor_load has not been called"; return QC_EINVAL; }
+    if (B < 0 || B > a->p.max_batch) { a->err = "B must be in [0, max_batch]"; return QC_EINVAL; }
+    if (B == 0) return QC_OK;
+    if (!obs || !actions) { a->err = "obs and actions are required"; return QC_EINVAL; }
+    Dev g(a->device);
+    const bool need_noise = noisy && (a->has_s[2] || a->has_s[3]);
+    if (need_noise) {
+        if (noise) {
+            const int64_t n = B * a->noise_len;
+            hipLaunchKernelGGL(k_actor_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, a->stream, noise,
+                               a->d_noise, a->p.max_batch, B, a->noise_len);
+        } else {
+            hipLaunchKernelGGL(k_actor_noise, dim3((unsigned)((B + 255) / 256), (unsigned)((a->noise_len + 1) / 2)),
+                               dim3(256), 0, a->stream, a->d_noise, a->p.max_batch, B, a->noise_len, env_offset,
+                               a->p.seed, counter);
+        }
+    }
+    ActArgs k{};
+    for (int l = 0; l < 4; ++l) {
+        k.L[l].u = a->d_w + a->off_u[l];
+        k.L[l].ub = a->d_w + a->off_ub[l];
+        k.L[l].s = a->has_s[l] ? a->d_w + a->off_s[l] : nullptr;
+        k.L[l].sb = a->has_s[l] ? a->d_w + a->off_sb[l] : nullptr;
+    }
+    k.in_len = a->p.data_length;
+    k.in_pad = a->in_pad;
+    k.n_act = a->p.n_actions;
+    k.B = B;
+    k.env_offset = env_offset;
+    k.obs = obs;
+    k.noisy = need_noise ? 1 : 0;
+    k.noise = a->d_noise;
+    k.noise_ld = a->p.max_batch;
+    k.eps = (float)eps;
+    k.seed = a->p.seed;
+    k.counter = counter;
+    k.actions = actions;
+    k.q_out = q_out;
+    k.random_out = random_out;
+    hipLaunchKernelGGL(k_actor_act, dim3((unsigned)((B + kE - 1) / kE)), dim3(kThreads),
+                       (2 * kH1 * kE + 16 * 64) * sizeof(float), a->stream, k);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(a, e, "actor launch");
+    return QC_OK;
+}
+
+}  // extern "C"

@@ -170,6 +170,60 @@ int qc_reset(qc_handle* h, void* psi, int32_t kind, const uint8_t* mask, double 
  * action a (forward, backward), and the truncation bound used. */
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);
 
+/* ---------------------------------------------------------------------------------------------
+ * Batched DQN actor: the reference's direct_DQN action selection
+ * (inverted harmonic oscillator/RL.py:80-111 + layers.py FactorizedNoisy / Linear_weight_normalize),
+ * evaluated for B envs at once on the device, with the actor's epsilon-greedy choice
+ * (IHO/main_parallel.py:208-219), replacing the per-actor pipe to the inference process
+ * (IHO/main_parallel.py:414-440). Layers: fc1 (in -> 512), fc2 (512 -> 256), fc31 (256 -> 256),
+ * fc41 (256 -> n_actions), ReLU between; actions = argmax of fc41 (the mean branch fc32/fc42 does not
+ * enter the action). fp32 throughout (the reference net's dtype), f32-input MFMA. */
+typedef struct qc_actor qc_actor;
+
+typedef struct qc_dqn_params {
+    int32_t data_length;   /* network input length (5 for the 'xp' input, IHO/main_parallel.py:137-138) */
+    int32_t n_actions;     /* 21 */
+    int64_t max_batch;     /* largest B passed to qc_actor_act */
+    uint64_t seed;         /* Philox key of the NoisyNet noise and the epsilon-greedy draws */
+} qc_dqn_params;
+
+/* One layer's parameters (device fp32 pointers, the reference state_dict tensors):
+ * Linear_weight_normalize: weight [out][in], bias [out], weight_norm (scalar g; effective weight
+ *   W g / ||W||_F, layers.py:97-103); sigma_w = sigma_b = NULL.
+ * FactorizedNoisy: weight = u_w [out][in], bias = u_b, sigma_w [out][in], sigma_b [out],
+ *   weight_norm = NULL (layers.py:7-79). */
+typedef struct qc_dqn_layer {
+    const float* weight;
+    const float* bias;
+    const float* weight_norm;
+    const float* sigma_w;
+    const float* sigma_b;
+} qc_dqn_layer;
+
+int qc_actor_create(const qc_dqn_params* p, int device, qc_actor** out);
+void qc_actor_destroy(qc_actor* a);
+const char* qc_actor_last_error(const qc_actor* a);
+int qc_actor_set_stream(qc_actor* a, void* stream);
+/* (re)load fc1, fc2, fc31, fc41 (the trainer's periodic state_dict push, IHO/main_parallel.py:400-405):
+ * computes the effective weights and stores them in the kernels' fragment order on the device */
+int qc_actor_load(qc_actor* a, const qc_dqn_layer layers[4]);
+
+/* Noise of the factorised noisy layers per env: eps_in(fc31)[256], eps_out(fc31)[256],
+ * eps_in(fc41)[256], eps_out(fc41)[n_actions], each f(z) = sign(z) sqrt|z| of a standard normal z
+ * (layers.py:77-79): qc_actor_noise_len() floats per env. */
+int qc_actor_noise_len(const qc_actor* a);
+
+/* One action per env: obs [B][data_length] fp32 (device): the network input exactly as the actor hands it
+ * over (get_data(state) * input_scaling in float32, IHO/main_parallel.py:131,241,247; BatchedEnv.obs),
+ * actions [B] int32 (device). noisy = 0 evaluates the mean weights
+ * (layers.py:41-43); noise NULL draws the NoisyNet noise in-kernel (Philox keyed by seed and
+ * env_offset + e, counter `counter`), else injected [B][noise_len] fp32. With probability eps an env
+ * takes a uniform random action instead (random_out[e] = 1). q_out [B][n_actions] fp32 and
+ * random_out [B] int32 are optional. */
+int qc_actor_act(qc_actor* a, int64_t B, int64_t env_offset, const float* obs, int32_t noisy,
+                 const float* noise, double eps, uint64_t counter, int32_t* actions, float* q_out,
+                 int32_t* random_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,63 @@
+"""CPU checks of the direct_DQN restatement (oracle/dqn.py) that the device actor is tested against."""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import dqn  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.actor import random_direct_dqn  # noqa: E402
+
+
+def test_random_params_follow_reference_init():
+    p = random_direct_dqn(seed=3)
+    assert p["fc1.weight"].shape == (512, 5) and p["fc2.weight"].shape == (256, 512)
+    assert p["fc31.u_w"].shape == (256, 256) and p["fc41.u_w"].shape == (21, 256)
+    assert float(p["fc31.u_w"].abs().max()) <= math.sqrt(6 / 256) + 1e-7
+    assert torch.allclose(p["fc41.sigma_w"], torch.full((21, 256), 0.5 / 16))
+    assert float(p["fc31.u_b"].abs().max()) == 0.0
+    assert math.isclose(float(p["fc2.weight_norm"]), float(p["fc2.weight"].norm()), rel_tol=1e-6)
+    q = random_direct_dqn(noisy_layers=0, seed=3)
+    assert "fc41.weight_norm" in q and "fc41.u_w" not in q
+
+
+def test_factorised_noise_equals_per_sample_weights():
+    """layers.py:45-58: w = u_w + sigma_w * bmm(rand_out, rand_in), b = u_b + sigma_b * rand_out,
+    output = baddbmm(b, x, w^T) -- restated with explicit per-sample weight matrices."""
+    g = torch.Generator().manual_seed(1)
+    n, i, o = 7, 256, 21
+    u, s = torch.randn(o, i, generator=g, dtype=torch.float64), torch.rand(o, i, generator=g, dtype=torch.float64)
+    ub, sb = torch.randn(o, generator=g, dtype=torch.float64), torch.rand(o, generator=g, dtype=torch.float64)
+    x = torch.randn(n, i, generator=g, dtype=torch.float64)
+    r_in = torch.randn(n, 1, i, generator=g, dtype=torch.float64)
+    r_out = torch.randn(n, o, 1, generator=g, dtype=torch.float64)
+    f = lambda z: torch.sign(z) * torch.sqrt(torch.abs(z))  # noqa: E731
+    e_in, e_out = f(r_in), f(r_out)
+    w = u + s * torch.bmm(e_out, e_in)
+    b = (ub + sb * e_out.squeeze(2)).unsqueeze(1)
+    ref = torch.baddbmm(b, x.view(n, 1, i), w.transpose(1, 2)).view(n, o).numpy()
+    got = dqn._apply(("noisy", u.numpy(), ub.numpy(), s.numpy(), sb.numpy()), x.numpy(),
+                     e_in.view(n, i).numpy(), e_out.view(n, o).numpy())
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_weight_normalised_linear():
+    """layers.py:101-103: F.linear(x, W / ||W|| * g, b)"""
+    g = torch.Generator().manual_seed(2)
+    w, b = torch.randn(512, 5, generator=g, dtype=torch.float64), torch.randn(512, generator=g, dtype=torch.float64)
+    gn = torch.tensor(3.7, dtype=torch.float64)
+    x = torch.randn(9, 5, generator=g, dtype=torch.float64)
+    ref = torch.nn.functional.linear(x, w / w.norm() * gn, b).numpy()
+    lay = dqn.layer({"l.weight": w, "l.bias": b, "l.weight_norm": gn}, "l")
+    np.testing.assert_allclose(dqn._apply(lay, x.numpy()), ref, rtol=1e-12, atol=1e-12)
+
+
+def test_forward_shapes_and_mean_path():
+    p = random_direct_dqn(seed=5)
+    obs = np.random.default_rng(0).standard_normal((4, 5))
+    q0 = dqn.forward(p, obs)
+    assert q0.shape == (4, 21)
+    zero = np.zeros((4, dqn.noise_len()))
+    np.testing.assert_allclose(dqn.forward(p, obs, zero), q0, rtol=1e-12, atol=1e-12)
+    assert dqn.noise_len() == 789

@@ -57,22 +57,38 @@ struct ActArgs {
     int32_t* random_out;
 };
 
-// acc += A_frag(W) . X  over `steps` k-steps (X: LDS [k][32]; lane reads X[2s + (lane>>5)][lane&31])
+// acc += A_frag(W) . X  over `steps` k-steps (X: LDS [k][32]; lane reads X[2s + (lane>>5)][lane&31]).
+// The weight fragments come from L2: batches of kP steps, the next batch's loads issued before the
+// current batch's MFMAs (kP x 64 cycles of MFMA cover the L2 latency at one wave per SIMD).
+constexpr int kP = 16;
 __device__ __forceinline__ void gemm_tile(f32x16& acc, const float* __restrict__ wf, const float* x, int steps,
                                           int lane) {
     const float* xl = x + (lane >> 5) * kE + (lane & 31);
     const float* wl = wf + lane;
-    int s = 0;
-    for (; s + 8 <= steps; s += 8) {
-        float a[8], b[8];
+    const int full = steps / kP * kP;
+    f32x16 acc1 = {};   // second accumulator chain (odd steps): halves the dependent-MFMA chain
+    float a[kP];
+    if (full > 0) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] = wl[(s + u) * 64];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) b[u] = xl[(s + u) * 2 * kE];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+        for (int u = 0; u < kP; ++u) a[u] = wl[u * 64];
     }
-    for (; s < steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[s * 64], xl[s * 2 * kE], acc, 0, 0, 0);
+    for (int s = 0; s < full; s += kP) {
+        float an[kP];
+        const int sn = s + kP < full ? s + kP : s;   // last batch: harmless reload of the same fragments
+#pragma unroll
+        for (int u = 0; u < kP; ++u) an[u] = wl[(sn + u) * 64];
+        __builtin_amdgcn_sched_barrier(0);   // keep the next batch's loads ahead of this batch's MFMAs
+#pragma unroll
+        for (int u = 0; u < kP; u += 2) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], xl[(s + u) * 2 * kE], acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u + 1], xl[(s + u + 1) * 2 * kE], acc1, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kP; ++u) a[u] = an[u];
+    }
+    for (int s = full; s < steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[s * 64], xl[s * 2 * kE], acc, 0, 0, 0);
+    acc += acc1;
 }
 
 // D-tile element r of this lane: output row (within the tile) and env column
@@ -204,9 +220,14 @@ __global__ __launch_bounds__(256) void k_actor_noise(float* out, int64_t ld, int
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int p = blockIdx.y;
     if (e >= B) return;
-    double z0, z1;
-    normals(seed, (uint32_t)(env_offset + e), counter, 0x100u + (uint32_t)p, z0, z1);
-    const float f0 = (float)z0, f1 = (float)z1;
+    // Box-Muller in fp32 (hardware log / sin / cos): the network noise is fp32 and has no oracle stream
+    uint32_t c[4] = {(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)(env_offset + e), 0x100u + (uint32_t)p};
+    philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = ((float)(c[0] >> 8) + 0.5f) * 0x1.0p-24f, u2 = (float)(c[1] >> 8) * 0x1.0p-24f;
+    const float rad = sqrtf(-2.f * __logf(u1));
+    float sn, cs;
+    __sincosf(6.283185307f * u2, &sn, &cs);
+    const float f0 = rad * cs, f1 = rad * sn;
     out[(int64_t)(2 * p) * ld + e] = copysignf(sqrtf(fabsf(f0)), f0);
     if (2 * p + 1 < noise_len) out[(int64_t)(2 * p + 1) * ld + e] = copysignf(sqrtf(fabsf(f1)), f1);
 }

@@ -441,11 +441,13 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.obs_out = obs_out;
     DeviceGuard g(h->device);
     if (h->p.batch == 0) return QC_OK;
-    if (actions) {
-        // group envs by force slot, padded to whole 4-env blocks: every block then shares one slot's
-        // tables (the per-block LDS image); order within a slot does not change any result
+    if (actions || env_steps) {
+        // group envs by force slot, padded to whole workgroups: every workgroup then shares one slot's
+        // tables (the per-block LDS image); envs without a step budget form a last group of their own
+        // (a reset interval of a few finished envs then costs in proportion to them); order within a
+        // group does not change any result
         const size_t W = (size_t)h->wpb;
-        const size_t cap = (size_t)((h->p.batch + W - 1) / W) * W + W * (size_t)kMaxSlots;
+        const size_t cap = (size_t)((h->p.batch + W - 1) / W) * W + W * (size_t)(kMaxSlots + 1);
         if (h->order_cap < cap) {
             if (h->d_order) (void)hipFree(h->d_order);
             h->d_order = nullptr;
@@ -454,7 +456,8 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
             h->order_cap = cap;
         }
-        if (launch_group(actions, h->p.batch, (int)h->acts.size(), (int)W, h->d_order, (int32_t)cap, h->stream))
+        if (launch_group(actions, default_action, env_steps, n_steps, h->p.batch, (int)h->acts.size(), (int)W,
+                         h->d_order, (int32_t)cap, h->stream))
             return fail(h, QC_EHIP, "group kernel launch failed");
         a.order = h->d_order;
         a.n_blocks = (uint32_t)(cap / W);

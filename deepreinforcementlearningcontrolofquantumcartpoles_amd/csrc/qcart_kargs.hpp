@@ -89,7 +89,7 @@ int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mas
 bool have_kernel(int family, int R, int precision = 0);
 int step_waves(int family, int R, int precision = 0);   // envs (waves) per step-kernel workgroup
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
-int launch_group(const int32_t* actions, int64_t B, int n_slots, int gran, int32_t* order, int32_t cap,
-                 void* stream);
+int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
+                 int n_slots, int gran, int32_t* order, int32_t cap, void* stream);
 
 }  // namespace qcart

@@ -908,7 +908,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     // H_F force coefficients from LDS (apply_hf_fx): fp64 Fock families with the tables in LDS
     constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8;
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
-    if constexpr (MODE >= 1) {
+    // a block of the no-budget group (k_group puts envs with env_steps <= 0 in whole blocks of their
+    // own) takes no step: it skips the table image
+    const bool block_idle = a.order && a.env_steps && (a.env_steps[e0] <= 0 || a.n_steps <= 0);
+    if (MODE >= 1 && !block_idle) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
         // the 4 waves for all n_steps steps
         char* img = (char*)smem_dyn;

@@ -442,3 +442,34 @@ def test_fp32_rejects_grid_and_wrong_dtype():
     st = Stepper(cfg.DEFAULTS[cfg.IHO].with_(n_max=511, precision=1), 2, 0)
     with pytest.raises(ValueError, match="Complex64"):
         st.step(torch.zeros((2, 512), dtype=torch.complex128, device="cuda"), None, 1)
+
+
+@pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513"])
+def test_env_steps_grouping_bitwise(case):
+    """Step budgets with per-env actions (the grouped path: no-budget envs in a workgroup group of their
+    own, k_group): frozen envs stay bitwise untouched, full-budget envs equal an unbudgeted call and
+    partial-budget envs equal a call of that many steps, bitwise."""
+    ph = CASES[case]
+    B = 100
+    st = Stepper(ph, B, 0, seed=21)
+    psi0 = st.new_state()
+    if ph.fock:
+        st.reset(psi0, 1, arg0=16)
+    else:
+        st.reset(psi0, 2, arg0=0.0, arg1=0.0, arg2=1.0)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    acts = torch.randint(0, 21, (B,), generator=g, device="cuda", dtype=torch.int32)
+    budget = torch.tensor([[0, 40, 80][i % 3] for i in range(B)], dtype=torch.int32, device="cuda")
+    a = psi0.clone()
+    out = st.step(a, acts, 80, env_steps=budget, want_fail=True)
+    st.step_counter = 0
+    full = psi0.clone()
+    st.step(full, acts, 80)
+    st.step_counter = 0
+    part = psi0.clone()
+    st.step(part, acts, 40)
+    bz = budget.cpu().numpy()
+    for e in range(B):
+        want = {0: psi0, 40: part, 80: full}[int(bz[e])]
+        assert torch.equal(a[e], want[e]), e
+    assert int(out["fail_step"][budget == 0].abs().sum()) == 0

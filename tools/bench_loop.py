@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""End-to-end actor loop on one GPU (SURVEY §8f rank 1 measured in place): BatchedEnv (IHO N = 512) +
+DQNActor (direct_DQN, random-initialised weights of the reference architecture) for K control steps:
+act -> step (80 physics steps) -> experience rows, with auto-reset of finished episodes.
+Prints one JSON line: RL steps/s (decisions), env-steps/s and the actor's share of the loop.
+usage: python tools/bench_loop.py [--batch B] [--steps K]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.actor import DQNActor, random_direct_dqn  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.env import BatchedEnv  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    B = args.batch
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)
+    env = BatchedEnv(ph, B, 0, seed=1)
+    actor = DQNActor({k: v.cuda() for k, v in random_direct_dqn(seed=1).items()}, max_batch=B, seed=2)
+    obs = env.reset()
+    steps_done = 0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    actor_ms = 0.0
+    rows = 0
+    for it in range(args.warmup + args.steps):
+        if it == args.warmup:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            actor_ms = 0.0
+            rows = 0
+        e0.record()
+        a = actor.act(obs, eps=DQNActor.eps_threshold(steps_done))
+        e1.record()
+        steps_done += B
+        obs, reward, done, info = env.step(a)
+        rows += int(info["valid"].sum())
+        BatchedEnv.experience(info["last_obs"], obs, a, reward)
+        e1.synchronize()
+        actor_ms += e0.elapsed_time(e1)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    K = args.steps
+    print(json.dumps({"metric": "actor loop RL steps/s (BatchedEnv IHO N=512 + device DQN actor)",
+                      "value": B * K / dt, "unit": "decisions/s", "env_steps_per_s": B * K * ph.control_interval / dt,
+                      "batch": B, "control_steps": K, "ms_per_control_step": dt / K * 1e3,
+                      "actor_ms_per_control_step": actor_ms / K, "actor_share": actor_ms / (dt * 1e3),
+                      "experience_rows_per_s": rows / dt,
+                      "data": "synthetic: |0> resets, random-initialised direct_DQN weights"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("QCART_LIB") or os.path.join(_HERE, "libqcart.so")
 QC_HO, QC_IHO, QC_QO, QC_IQO = 0, 1, 2, 3
 QC_A_REFERENCE, QC_A_EXACT = 0, 1
 QC_RESET_GROUND, QC_RESET_RANDOM, QC_RESET_GAUSSIAN = 0, 1, 2
+QC_CTL_LQG, QC_CTL_DAMPING, QC_CTL_SEMICLASSICAL = 0, 1, 2
+CONTROL_STRATEGIES = {"LQG": QC_CTL_LQG, "damping": QC_CTL_DAMPING, "semiclassical": QC_CTL_SEMICLASSICAL}
 
 STATUS = {
     0: "QC_OK", -1: "QC_EINVAL", -2: "QC_ENOMEM", -3: "QC_EHIP", -4: "QC_EPIVOT", -5: "QC_ESINGULAR",
@@ -26,7 +28,7 @@ EXPORTS = (
     "qc_create", "qc_destroy", "qc_last_error", "qc_abi_version", "qc_get_params", "qc_dim", "qc_n_obs",
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
-    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_scan_levels",
+    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_scan_levels",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
 )
@@ -128,6 +130,7 @@ def lib() -> ctypes.CDLL:
     L.qc_energy.argtypes = [vp, vp, vp]
     L.qc_phonon_number.argtypes = [vp, vp, vp]
     L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
+    L.qc_control.argtypes = [vp, vp, i32, d, d, d, vp, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
     L.qc_actor_create.argtypes = [P(QcDqnParams), ctypes.c_int, P(vp)]
     L.qc_actor_destroy.argtypes = [vp]

@@ -200,6 +200,22 @@ class Stepper:
         L.check(L.lib().qc_phonon_number(self._h, _ptr(psi), _ptr(out)), self._h)
         return out
 
+    def control(self, psi: torch.Tensor, strategy: str | int = "LQG", con_parameter: float = 0.0,
+                control_time: float | None = None, input_scaling: float = 1.0):
+        """Analytic baseline controller per env (qc_control): returns (actions int32 [B], force fp64 [B]).
+        strategy: 'LQG' (Fock args.LQG; grid LinearQuadratic), 'damping', 'semiclassical' (grid).
+        control_time defaults to 1 / n_con (IHO/main_parallel.py:195, QO/controllers.py:5)."""
+        self._check_psi(psi)
+        s = L.CONTROL_STRATEGIES[strategy] if isinstance(strategy, str) else int(strategy)
+        if control_time is None:
+            control_time = 1.0 / self.physics.n_con
+        act = torch.empty((self.batch,), dtype=torch.int32, device=self.device)
+        force = torch.empty((self.batch,), dtype=torch.float64, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_control(self._h, _ptr(psi), s, float(con_parameter), float(control_time),
+                                   float(input_scaling), _ptr(act), _ptr(force)), self._h)
+        return act, force
+
     def reset(self, psi: torch.Tensor, kind: int, mask: Optional[torch.Tensor] = None, arg0: float = 0.0,
               arg1: float = 0.0, arg2: float = 1.0, k: Optional[torch.Tensor] = None,
               mean: Optional[torch.Tensor] = None, std: Optional[torch.Tensor] = None):

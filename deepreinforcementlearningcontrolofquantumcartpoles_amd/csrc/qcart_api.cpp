@@ -540,6 +540,35 @@ int qc_reset(qc_handle* h, void* psi, int32_t kind, const uint8_t* mask, double 
     return rc ? fail(h, rc, "reset kernel launch failed") : QC_OK;
 }
 
+int qc_control(qc_handle* h, const void* psi, int32_t strategy, double con_parameter, double control_time,
+               double input_scaling, int32_t* actions, double* force_out) {
+    if (!h || (!psi && h->p.batch > 0) || (!actions && h->p.batch > 0)) return QC_EINVAL;
+    if (strategy < QC_CTL_LQG || strategy > QC_CTL_SEMICLASSICAL) return fail(h, QC_EINVAL, "bad control strategy");
+    if (h->op.fock && strategy != QC_CTL_LQG)
+        return fail(h, QC_EINVAL, "the Fock families define the LQG controller only");
+    if (!(control_time > 0)) return fail(h, QC_EINVAL, "control_time must be > 0");
+    // LinearQuadratic takes sqrt(k * mass), k = lambda * con_parameter (controllers.py:20): the
+    // reference raises a math domain error when that is negative
+    if (!h->op.fock && strategy == QC_CTL_LQG && h->p.lambda_ * con_parameter * h->p.mass < 0)
+        return fail(h, QC_EINVAL, "LQG: lambda * con_parameter * mass < 0 (math domain error)");
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    a.act_out = actions;
+    a.force_out = force_out;
+    a.ctl_strategy = strategy;
+    a.ctl_param = con_parameter;
+    a.ctl_time = control_time;
+    a.ctl_scaling = input_scaling;
+    a.ctl_half = h->p.n_actions / 2;
+    // force_max = net.convert_to_force(2 * no_action_choice) = round(2h - h) * (F_max / h) (RL.py:107-109)
+    a.ctl_fmax = (double)a.ctl_half * (h->p.f_max / a.ctl_half);
+    a.ctl_lambda = h->p.lambda_;
+    a.ctl_mass = h->p.mass;
+    DeviceGuard g(h->device);
+    int rc = launch_control(h->p.family, h->R, a, h->stream);
+    return rc ? fail(h, rc, "control kernel launch failed") : QC_OK;
+}
+
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {
     if (!h || action < 0 || action >= (int)h->acts.size()) return QC_EINVAL;
     if (fwd) *fwd = h->acts[action].kf;

@@ -61,6 +61,9 @@ int launch_obs(int family, int R, const KArgs& a, void* stream) {
 int launch_aux(int family, int R, int what, const KArgs& a, double xth, void* out, void* stream) {
     return route(family, R, 2, a, what, xth, out, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, stream);
 }
+int launch_control(int family, int R, const KArgs& a, void* stream) {
+    return route(family, R, 5, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, stream);
+}
 int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mask, double a0, double a1, double a2,
                  const double* k_arr, const double* m_arr, const double* s_arr, void* stream) {
     return route(family, R, 3, a, 0, 0.0, nullptr, kind, mask, a0, a1, a2, k_arr, m_arr, s_arr, stream);

@@ -76,6 +76,12 @@ struct KArgs {
     const int32_t* kf;         // [slot]
     const int32_t* kb;         // [slot]
     const double* force;       // [slot]
+    // analytic controllers (qc_control)
+    int32_t* act_out;          // [B]
+    double* force_out;         // [B] or null
+    int32_t ctl_strategy;      // enum qc_control_strategy
+    int32_t ctl_half;          // no_action_choice (10)
+    double ctl_param, ctl_time, ctl_scaling, ctl_fmax, ctl_lambda, ctl_mass;
 };
 
 // host-side launchers (qcart_kernels.hip)
@@ -86,6 +92,7 @@ int launch_aux(int family, int R, int what, const KArgs& a, double xth, void* ou
 int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mask, double a0,
                  double a1, double a2, const double* k_arr, const double* m_arr, const double* s_arr,
                  void* stream);
+int launch_control(int family, int R, const KArgs& a, void* stream);   // qc_control (act_out / force_out)
 bool have_kernel(int family, int R, int precision = 0);
 int step_waves(int family, int R, int precision = 0);   // envs (waves) per step-kernel workgroup
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip

@@ -1375,6 +1375,109 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
     }
 }
 
+// ---- analytic controllers -------------------------------------------------
+// grid p_hat of the drivers' space_def.py:13-21,59 (the Python operator the controllers use): the full
+// antisymmetric 8th-order Delta_1 band (every entry whose column lies in [0, N)), p = -i Delta_1.
+template <int R>
+__device__ __forceinline__ void grid_p_full(const cd (&v)[R], cd (&o)[R], double inv_h, int N, int base, int lane) {
+    cd e[R + 8];
+    make_ext<R, 4>(v, e, lane);   // rows outside [0, N) are zero in v and in the halo
+    const double sd[5] = {0.0, 672.0 / 840.0, -168.0 / 840.0, 32.0 / 840.0, -3.0 / 840.0};
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int d = 1; d <= 4; ++d) {
+            re += sd[d] * inv_h * (e[4 + j + d].re - e[4 + j - d].re);
+            im += sd[d] * inv_h * (e[4 + j + d].im - e[4 + j - d].im);
+        }
+        o[j] = (base + j < N) ? C(im, -re) : C(0.0, 0.0);   // -i (re + i im)
+    }
+}
+
+// action from the controller's force (HO/main_parallel.py:196-203, IHO/main_parallel.py:197-206,
+// QO/main_parallel.py:175-181): clip to +-force_max, Python round() to the action grid (ties to even)
+__device__ __forceinline__ void ctl_round(double force, double fm, int half, int32_t& act, double& f_out) {
+    force = fmin(force, fm);
+    force = fmax(force, -fm);
+    const double step = fm / half;
+    f_out = rint(force / step) * step;
+    act = (int32_t)rint(f_out / step) + half;
+}
+
+// qc_control: one wave per env. Fock (HO / IHO) LQG on the network input data = float32(get_data_xp)
+// * input_scaling (x = data[0], p = data[1]; x + p in float32, the rest in fp64 as numpy 1.x promotes
+// a float32 scalar times a Python float); grid damping / LQG / semiclassical (controllers.py:7-29) on
+// <x>, <p>, <x^2>, <x^3>, Re<x p x> of the state with the space_def operators.
+template <int FAM, int R, typename RT = double>
+__global__ __launch_bounds__(256) void k_control(const KArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (env >= a.B) return;
+    const int base = lane * R, N = a.N;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+    const size_t e0 = (size_t)env * N;
+    cd psi[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld_psi<RT>(a.psi, e0 + base + j) : C(0.0, 0.0);
+    const double T = a.ctl_time;
+    double F;
+    if constexpr (FAM <= 1) {
+        double o[5];
+        fock_obs<FAM, R>(psi, cf, lane, o);
+        const float sc = (float)a.ctl_scaling;
+        const float x = (float)o[0] * sc, p = (float)o[1] * sc;
+        const double w = a.c;   // omega
+        if constexpr (FAM == 1)   // IHO/main_parallel.py:197
+            F = (double)(-(x + p)) * (1.0 + w * T + 0.5 * w * w * T * T) / (T + w * T * T / 2.0);
+        else                      // HO/main_parallel.py:197
+            F = -((double)(x + p) + (double)(p - x) * w * T) / T;
+        F = F / w;
+    } else {
+        const double h = a.h, inv_h = 1.0 / h;
+        cd pv[R], xv[R], pxv[R];
+        grid_p_full<R>(psi, pv, inv_h, N, base, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) xv[j] = C(cf.xg[j] * psi[j].re, cf.xg[j] * psi[j].im);
+        grid_p_full<R>(xv, pxv, inv_h, N, base, lane);
+        double s[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double x = cf.xg[j], n2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+            s[0] += x * n2;
+            s[1] += psi[j].re * pv[j].re + psi[j].im * pv[j].im;
+            s[2] += x * x * n2;
+            s[3] += x * x * x * n2;
+            s[4] += xv[j].re * pxv[j].re + xv[j].im * pxv[j].im;   // Re conj(psi) x p (x psi)
+        }
+        wave_sum<5>(s);
+        const double xe = s[0] * h, pe = s[1] * h, x2 = s[2] * h, x3 = s[3] * h, xpx = s[4] * h;
+        const double lam = a.ctl_lambda, m = a.ctl_mass;
+        if (a.ctl_strategy == 1) {   // steepest_descent(predict_evolution=True, damping), controllers.py:7-14
+            const double pp = pe - 4. * lam * x3 * T - T * T * 2. * lam * 3. * xpx / m;
+            F = -pp / T * a.ctl_param;
+        } else if (a.ctl_strategy == 0) {   // LinearQuadratic(k = lambda * con_parameter), :16-20
+            const double k = lam * a.ctl_param;
+            const double xq = xe + pe / m * T - T * T * 2. * lam * x3 / m;
+            const double pq = pe - 4. * lam * x3 * T - T * T * 2. * lam * 3. * xpx / m;
+            F = -(sqrt(k * m) * xq + pq) / T;
+        } else {   // Gaussian_approx, :22-29
+            const double var = x2 - xe * xe;
+            const double tp = -sqrt(2 * m * (6 * lam * var + lam * xe * xe)) * xe;   // < 0 under the root: NaN
+            F = (tp - pe) / T;
+        }
+        F = F / M_PI;   // force = F / pi (QO/main_parallel.py:176)
+    }
+    if (lane == 0) {
+        int32_t act = -1;   // NaN force: the reference raises (math domain error); reported as action -1
+        double f = F;
+        if (!isnan(F)) ctl_round(F, a.ctl_fmax, a.ctl_half, act, f);
+        a.act_out[env] = act;
+        if (a.force_out) a.force_out[env] = f;
+    }
+}
+
 template <int FAM, int R, typename RT = double>
 __global__ __launch_bounds__(256) void k_reset(const KArgs a, int kind, const uint8_t* mask, double a0, double a1,
                                                 double a2, const double* k_arr, const double* m_arr,
@@ -1468,6 +1571,7 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     }
     else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);
     else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R, RT>), grid, block, 0, st, a, what, xth, out);
+    else if (kind == 5) hipLaunchKernelGGL((k_control<FAM, R, RT>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_reset<FAM, R, RT>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

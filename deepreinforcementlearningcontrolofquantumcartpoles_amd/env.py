@@ -185,6 +185,13 @@ class BatchedEnv:
                 self.reset(done)
         return self.obs, reward.to(torch.float32), done, info
 
+    def analytic_actions(self, strategy: str = "LQG", con_parameter: float = 0.0) -> torch.Tensor:
+        """Actions of the reference's analytic baseline controllers for the current states (qc_control):
+        Fock args.LQG on the 'xp' network input (IHO/main_parallel.py:194-206), grid
+        args.control_strategy in {'LQG', 'damping', 'semiclassical'} (QO/main_parallel.py:165-181)."""
+        act, _ = self.st.control(self.psi, strategy, con_parameter, input_scaling=self.input_scaling)
+        return act
+
     @staticmethod
     def experience(last_obs: torch.Tensor, obs: torch.Tensor, action: torch.Tensor, reward: torch.Tensor):
         """Experience rows in the reference layout np.hstack((last_data, data, [last_action], [reward]))."""

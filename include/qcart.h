@@ -166,6 +166,25 @@ enum qc_reset_kind { QC_RESET_GROUND = 0, QC_RESET_RANDOM = 1, QC_RESET_GAUSSIAN
 int qc_reset(qc_handle* h, void* psi, int32_t kind, const uint8_t* mask, double arg0, double arg1,
              double arg2, const double* k_arr, const double* mean_arr, const double* std_arr);
 
+/* Analytic baseline controllers, one action per env from the current state:
+ *   QC_CTL_LQG           Fock: the actor's args.LQG branch of call_force (IHO/main_parallel.py:194-206,
+ *                        HO/main_parallel.py:192-203) on the network input data = float32 get_data_xp(state)
+ *                        * input_scaling (pass 1.0 for the unscaled get_data_xp of a non-'xp' input,
+ *                        IHO/main_parallel.py:261-262); control_time = 1 / n_con.
+ *                        grid: controllers.LinearQuadratic(state, k = lambda_ * con_parameter)
+ *                        (QO/controllers.py:16-20, QO/main_parallel.py:168)
+ *   QC_CTL_DAMPING       grid: controllers.steepest_descent(state, damping = con_parameter) (:7-14)
+ *   QC_CTL_SEMICLASSICAL grid: controllers.Gaussian_approx(state) (:22-29)
+ * Grid forces use the drivers' space_def operators (full Delta_1 p_hat) and control_time =
+ * 1 / controls_per_unit_time; force = F / pi (Fock: F / omega) is clipped to +-F_max and rounded to the
+ * action grid with Python round() semantics (analytic_controls, QO/main_parallel.py:170-181).
+ * actions [B] int32 (device) receive round(force / spacing) + n_actions/2; force_out [B] fp64 (optional)
+ * the rounded force passed to step(). A NaN force (Gaussian_approx with a negative root argument,
+ * where the reference raises a math domain error) yields action -1 and force NaN. */
+enum qc_control_strategy { QC_CTL_LQG = 0, QC_CTL_DAMPING = 1, QC_CTL_SEMICLASSICAL = 2 };
+int qc_control(qc_handle* h, const void* psi, int32_t strategy, double con_parameter, double control_time,
+               double input_scaling, int32_t* actions, double* force_out);
+
 /* Host-side introspection of the factor tables (tests): number of Kogge-Stone levels kept for
  * action a (forward, backward), and the truncation bound used. */
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);

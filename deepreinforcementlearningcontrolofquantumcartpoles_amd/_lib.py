@@ -28,7 +28,8 @@ EXPORTS = (
     "qc_create", "qc_destroy", "qc_last_error", "qc_abi_version", "qc_get_params", "qc_dim", "qc_n_obs",
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
-    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_scan_levels",
+    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_record_row_len", "qc_record",
+    "qc_scan_levels",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
 )
@@ -131,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.qc_phonon_number.argtypes = [vp, vp, vp]
     L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
     L.qc_control.argtypes = [vp, vp, i32, d, d, d, vp, vp]
+    L.qc_record_row_len.argtypes = [i32, i32, i32]
+    L.qc_record.argtypes = [vp, i32, i32, d, vp, i32, vp, i32, vp, vp, vp, vp, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
     L.qc_actor_create.argtypes = [P(QcDqnParams), ctypes.c_int, P(vp)]
     L.qc_actor_destroy.argtypes = [vp]

@@ -569,6 +569,47 @@ int qc_control(qc_handle* h, const void* psi, int32_t strategy, double con_param
     return rc ? fail(h, rc, "control kernel launch failed") : QC_OK;
 }
 
+int qc_record_row_len(int32_t read_length, int32_t interval, int32_t coarse_grain) {
+    if (read_length <= 0 || interval <= 0 || coarse_grain <= 0 || interval % coarse_grain) return QC_EINVAL;
+    const int m = interval / coarse_grain;
+    if (read_length % m) return QC_EINVAL;
+    return read_length + m + read_length / m + 1 + 2;
+}
+
+int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double input_scaling, const double* q,
+              int32_t n_steps, const int32_t* actions, int32_t default_action, const uint8_t* mode, float* hist,
+              float* forces, const float* reward, float* rows) {
+    if (!h) return QC_EINVAL;
+    const int row_len = qc_record_row_len(read_length, n_steps, coarse_grain);
+    if (row_len < 0)
+        return fail(h, QC_EINVAL, "need n_steps % coarse_grain == 0 and read_length % (n_steps / coarse_grain) == 0");
+    if (h->p.batch > 0 && (!q || !hist || !forces)) return fail(h, QC_EINVAL, "q, hist and forces are required");
+    if (!actions && (default_action < 0 || default_action >= (int)h->acts.size()))
+        return fail(h, QC_EINVAL, "default_action out of range");
+    RecArgs a{};
+    a.q = q;
+    a.actions = actions;
+    a.default_action = default_action;
+    a.slot_force = h->d_force;
+    a.mode = mode;
+    a.hist = hist;
+    a.forces = forces;
+    a.rows = rows;
+    a.reward = reward;
+    a.B = h->p.batch;
+    a.L = read_length;
+    a.cg = coarse_grain;
+    a.m = n_steps / coarse_grain;
+    a.K = read_length / a.m;
+    a.row_len = row_len;
+    a.scaling = input_scaling;
+    a.vec4 = (read_length % 4 == 0 && a.m % 4 == 0 && ((uintptr_t)hist & 15) == 0) ? 1 : 0;
+    if (sizeof(float) * (size_t)(2 * a.L + a.K + 1) > 160 * 1024) return fail(h, QC_EINVAL, "read_length too large");
+    DeviceGuard g(h->device);
+    int rc = launch_record(a, h->stream);
+    return rc ? fail(h, rc, "record kernel launch failed") : QC_OK;
+}
+
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {
     if (!h || action < 0 || action >= (int)h->acts.size()) return QC_EINVAL;
     if (fwd) *fwd = h->acts[action].kf;

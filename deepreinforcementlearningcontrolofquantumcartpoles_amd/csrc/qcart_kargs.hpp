@@ -84,6 +84,24 @@ struct KArgs {
     double ctl_param, ctl_time, ctl_scaling, ctl_fmax, ctl_lambda, ctl_mass;
 };
 
+// measurement-record update (qcart_record.hip, qc_record)
+struct RecArgs {
+    const double* q;            // [n_steps][B] step() q outputs of the interval
+    const int32_t* actions;     // [B] or null (default_action)
+    int32_t default_action;
+    const double* slot_force;   // [slot] force of each action slot
+    const uint8_t* mode;        // [B] 0 frozen, 1 record, 2 record into a fresh (zero) history; null = 1
+    float* hist;                // [B][2][L] in place
+    float* forces;              // [B][K + 1] in place
+    float* rows;                // [B][row_len] or null
+    const float* reward;        // [B] or null
+    int64_t B;
+    int32_t L, m, K, cg, row_len;
+    int32_t vec4;               // L, m multiples of 4: float4 history traffic
+    double scaling;
+};
+int launch_record(const RecArgs& a, void* stream);
+
 // host-side launchers (qcart_kernels.hip)
 // (the kernel precision is a.precision)
 int launch_step(int family, int R, const KArgs& a, void* stream);

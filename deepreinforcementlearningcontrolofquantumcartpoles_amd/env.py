@@ -8,14 +8,18 @@ Reference semantics reproduced per family ('xp' observation input):
       - done when the boundary Fail flag fired during the interval (numerical_failure) or, at the
         control step, |<x>| > xth = F_max (IHO) / the outside probability exceeded 0.5 at any
         physics step (IQO, checked every step); reward row value 1 (alive) or failing_reward (-1)
-  * cooling (HO, QO): HO/main_parallel.py:224-260, QO/main_parallel.py:169-232
+  * cooling (HO, QO): HO/main_parallel.py:222-292, QO/main_parallel.py:169-232
       - reset: HO |0>; QO Gaussian(k ~ U[-0.3,0.3]) evolved U[15,20] time units at F = 0, redrawn
         until energy < 7.5 and no Fail (QO/main_parallel.py:177-198)
-      - first decision at i = 0; at each control step the transition is stored with reward
+      - first decision at i = control_interval after a zero-force interval (HO:238, like the
+        cartpoles) / at i = 0 (QO:208); at each control step the transition is stored with reward
         -phonon*scale (HO) / -energy*scale (QO) while phonon <= cutoff / energy < cutoff and no Fail;
         otherwise the episode ends without storing it; the episode is truncated at t_max = 100
 The experience row layout is the reference's: [last_obs, obs, last_action, reward]
-(IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged.
+(IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged. With input='measurements'
+(HO, IHO; IHO/main_parallel.py:143-151,270-309) the observation is the device measurement record
+[B][2][read_length] (measurements.MeasurementRecord, updated in place by the qc_record kernel) and the
+experience rows [B][row_len] come from the same kernel (info['rows']).
 """
 from __future__ import annotations
 
@@ -25,6 +29,7 @@ import torch
 
 from . import config as cfg
 from .core import Stepper
+from .measurements import MeasurementRecord
 
 
 class BatchedEnv:
@@ -32,7 +37,7 @@ class BatchedEnv:
                  env_offset: int = 0, input_scaling: float = 1.0, failing_reward: float = -1.0,
                  reward_multiply: float = 1.0, t_max: float = 100.0, phonon_cutoff: float = 20.0,
                  energy_cutoff: float = 12.0, init_energy_cutoff: float = 7.5, auto_reset: bool = True,
-                 reset_kind: str = "reference"):
+                 reset_kind: str = "reference", input: str = "xp", read_length: Optional[int] = None):
         self.ph = physics
         self.B = int(batch)
         self.st = Stepper(physics, self.B, device, seed=seed, env_offset=env_offset)
@@ -50,12 +55,23 @@ class BatchedEnv:
         self.auto_reset = auto_reset
         self.reset_kind = reset_kind
         self.cartpole = physics.family in (cfg.IHO, cfg.IQO)
+        # no control at the zero-th step: the first decision follows one zero-force interval (IHO:250,
+        # IQO:201, HO:238); QO decides at i = 0 (QO:208)
+        self.first_interval = physics.family != cfg.QO
+        if input not in ("xp", "measurements"):
+            raise ValueError("input must be 'xp' or 'measurements'")
+        self.input = input
+        self.rec = None
+        if input == "measurements":
+            self.rec = MeasurementRecord(self.st, read_length, input_scaling=input_scaling)
+            self.rows = torch.empty((self.B, self.rec.row_len), dtype=torch.float32, device=self.dev)
         self.gen = torch.Generator(device=self.dev).manual_seed(int(seed) * 7919 + int(env_offset))
         z = lambda dt: torch.zeros(self.B, dtype=dt, device=self.dev)  # noqa: E731
         self.t = z(torch.float64)                 # episode time
         self.steps = z(torch.int64)               # physics steps in the episode
         self.last_action = torch.full((self.B,), self.half, dtype=torch.int32, device=self.dev)
-        self.obs = torch.zeros((self.B, self.st.n_obs), dtype=torch.float32, device=self.dev)
+        self.obs = (self.rec.hist if self.rec is not None else
+                    torch.zeros((self.B, self.st.n_obs), dtype=torch.float32, device=self.dev))
         self.episode_return = z(torch.float64)
         self.finished_returns: list = []          # (return, length) of finished episodes (host)
 
@@ -115,26 +131,34 @@ class BatchedEnv:
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
         self.episode_return = torch.where(mask, torch.zeros_like(self.episode_return), self.episode_return)
         self.last_action = torch.where(mask, torch.full_like(self.last_action, self.half), self.last_action)
-        if self.cartpole:
-            # no control at the zero-th step: one zero-force interval first (IHO:242-268, IQO:190-221).
-            # An episode that already ends at i = control_interval stores nothing (i != control_interval
-            # guard, IHO:250) and is simply restarted here.
+        if self.first_interval:
+            # no control at the zero-th step: one zero-force interval first (IHO:242-268, IQO:190-221,
+            # HO:237-257). An episode that already ends at i = control_interval stores nothing
+            # (i != control_interval guard, IHO:250) and is simply restarted here.
+            fam = self.ph.family
             todo = mask.clone()
             while bool(todo.any()):
                 budget = torch.where(todo, torch.full_like(self.last_action, self.ci), torch.zeros_like(self.last_action))
                 out = self.st.step(self.psi, None, self.ci, default_action=self.half, env_steps=budget,
-                                   want_term=(self.ph.family == cfg.IQO), want_obs=True)
+                                   want_term=(fam == cfg.IQO), want_obs=True, want_q=self.rec is not None)
+                if self.rec is not None:   # the record starts at i = 0 from empty lists (IHO:271-272)
+                    self.rec.record(out["q"], None, self.half, mode=todo.to(torch.uint8) * 2)
                 bad = out["fail_step"] > 0
-                if self.ph.family == cfg.IQO:
+                if fam == cfg.IQO:
                     bad |= out["term_step"] >= 0
-                else:
+                elif fam == cfg.IHO:
                     bad |= out["obs"][:, 0].abs() > self.ph.xth
+                else:   # HO: phonon > cutoff at the first control step ends the episode (HO:240-246)
+                    bad |= self.st.phonon_number(self.psi) > self.phonon_cutoff
                 bad &= todo
                 if bool(bad.any()):
                     self._reset_states(bad)
                 todo = bad
             self.t = torch.where(mask, self.t + self.ci * self.ph.dt, self.t)
             self.steps = torch.where(mask, self.steps + self.ci, self.steps)
+        if self.rec is not None:
+            self.obs = self.rec.hist
+            return self.obs
         obs = self._observe()
         self.obs = torch.where(mask[:, None], obs, self.obs)
         return self.obs
@@ -148,7 +172,7 @@ class BatchedEnv:
         last_obs = self.obs
         fam = self.ph.family
         out = self.st.step(self.psi, actions, self.ci, want_fail=True, want_obs=True,
-                           want_term=(fam == cfg.IQO))
+                           want_term=(fam == cfg.IQO), want_q=self.rec is not None)
         fail = out["fail_step"] > 0
         obs = out["obs"].to(torch.float32) * self.input_scaling
         self.t = self.t + self.ci * self.ph.dt
@@ -173,11 +197,17 @@ class BatchedEnv:
             numerical = fail
         self.episode_return = self.episode_return + torch.where(valid, reward, torch.zeros_like(reward))
         info = {"valid": valid, "numerical_failure": numerical & done, "t": self.t.clone(),
-                "last_obs": last_obs, "fail_step": out["fail_step"]}
+                "last_obs": last_obs if self.rec is None else None, "fail_step": out["fail_step"]}
+        if self.rec is not None:
+            # the continuous record of the two control steps, forces and (action, reward) (IHO:270-283)
+            self.rec.record(out["q"], actions, self.half, reward=reward.to(torch.float32), rows=self.rows)
+            info["rows"] = self.rows
+            obs = self.rec.hist
         self.last_action = actions
         self.obs = obs
         if bool(done.any()):
-            info["terminal_obs"] = obs.clone()
+            if self.rec is None:   # measurement mode: the rows hold the terminal record
+                info["terminal_obs"] = obs.clone()
             info["episode_return"] = self.episode_return.clone()
             info["episode_length"] = self.t.clone()
             self.finished_returns.append((self.episode_return[done].cpu(), self.t[done].cpu()))
@@ -189,7 +219,10 @@ class BatchedEnv:
         """Actions of the reference's analytic baseline controllers for the current states (qc_control):
         Fock args.LQG on the 'xp' network input (IHO/main_parallel.py:194-206), grid
         args.control_strategy in {'LQG', 'damping', 'semiclassical'} (QO/main_parallel.py:165-181)."""
-        act, _ = self.st.control(self.psi, strategy, con_parameter, input_scaling=self.input_scaling)
+        # the 'xp' input hands the scaled network input to call_force; other inputs pass the unscaled
+        # get_data_xp(state) (IHO:259-262)
+        sc = self.input_scaling if self.input == "xp" else 1.0
+        act, _ = self.st.control(self.psi, strategy, con_parameter, input_scaling=sc)
         return act
 
     @staticmethod

@@ -185,6 +185,28 @@ enum qc_control_strategy { QC_CTL_LQG = 0, QC_CTL_DAMPING = 1, QC_CTL_SEMICLASSI
 int qc_control(qc_handle* h, const void* psi, int32_t strategy, double con_parameter, double control_time,
                double input_scaling, int32_t* actions, double* force_out);
 
+/* Measurement-record input mode: args.input == 'measurements' of the Fock drivers
+ * (IHO/main_parallel.py:143-151,270-309; HO/main_parallel.py:142-150,259-292), for B envs in place on
+ * the device. Per env (device float32):
+ *   hist   [B][2][read_length]  the network input np.array([measurements_input[::-1],
+ *                               forces_along_measurements_input[::-1]]): measurements newest first, and
+ *                               force * input_scaling applied during each
+ *   forces [B][K + 1]           forces_to_store after the control step's append, newest first,
+ *                               K = read_length / m, m = n_steps / coarse_grain
+ * One call closes one control interval of n_steps physics steps: q [n_steps][B] fp64 are the q outputs of
+ * qc_step for it (q_out), actions [B] (or default_action) the actions applied during it. Each group of
+ * coarse_grain steps adds sum(q) / coarse_grain * input_scaling; the histories shift by m.
+ * mode [B] (device uint8, NULL = all 1): 0 leaves the env untouched, 1 records, 2 records into a fresh
+ * (zero) history (a new episode, IHO:271-272). rows [B][qc_record_row_len()] (optional) receive the
+ * experience row hstack(measurements_input[::-1] (read_length + m), forces_to_store[::-1] (K + 1),
+ * last_action, reward) (IHO:279-283, TrainDQN reads it at RL.py:180-192); the reward column is written
+ * only when reward [B] is given. The drivers' values: read_length = round(n_periods * 2 * 1440) with
+ * n_periods 2 (IHO, 5760) or 1.5 (HO, 4320), coarse_grain = time_steps / 1440. */
+int qc_record_row_len(int32_t read_length, int32_t interval, int32_t coarse_grain);
+int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double input_scaling, const double* q,
+              int32_t n_steps, const int32_t* actions, int32_t default_action, const uint8_t* mode, float* hist,
+              float* forces, const float* reward, float* rows);
+
 /* Host-side introspection of the factor tables (tests): number of Kogge-Stone levels kept for
  * action a (forward, backward), and the truncation bound used. */
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);

@@ -89,6 +89,10 @@ def test_batched_env_iqo_and_cooling_run():
         o, r, d, info = env.step(torch.full((8,), 10, dtype=torch.int32, device="cuda"))
     ho = BatchedEnv(cfg.DEFAULTS[cfg.HO], 8, 0, seed=1)
     o = ho.reset()
-    assert torch.allclose(o[:, 2], torch.full((8,), 0.5, device="cuda"))       # |0>: Var x = 1/2
+    # |0> then the zero-force first interval (HO:238): the measurement narrows Var x below 1/2, and
+    # for a Gaussian state the conditional variance is noise independent (same in every env)
+    assert torch.allclose(ho.t, torch.full((8,), ho.ci * ho.ph.dt, dtype=torch.float64, device="cuda"))
+    assert bool((o[:, 2] < 0.5).all()) and torch.allclose(o[:, 2], o[0, 2].expand(8), atol=1e-4)
+    assert not torch.allclose(o[:, 0], o[0, 0].expand(8))                     # <x> is noise driven
     o, r, d, info = ho.step(torch.full((8,), 10, dtype=torch.int32, device="cuda"))
     assert torch.all(r <= 0) and not bool(d.any())

@@ -32,6 +32,9 @@ EXPORTS = (
     "qc_scan_levels",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
+    "qc_replay_create", "qc_replay_destroy", "qc_replay_last_error", "qc_replay_set_stream", "qc_replay_store",
+    "qc_replay_store_xp", "qc_replay_sample", "qc_replay_update", "qc_replay_rebuild", "qc_replay_stats",
+    "qc_replay_buffers",
 )
 
 
@@ -74,6 +77,34 @@ class QcDqnLayer(ctypes.Structure):
         ("weight_norm", ctypes.c_void_p),
         ("sigma_w", ctypes.c_void_p),
         ("sigma_b", ctypes.c_void_p),
+    ]
+
+
+class QcReplayParams(ctypes.Structure):
+    _fields_ = [
+        ("capacity", ctypes.c_int64),
+        ("row_len", ctypes.c_int32),
+        ("policy", ctypes.c_int32),
+        ("passes_before_random", ctypes.c_double),
+        ("alpha", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("beta_increment", ctypes.c_double),
+        ("abs_err_upper", ctypes.c_double),
+        ("epsilon_scale", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class QcReplayStats(ctypes.Structure):
+    _fields_ = [
+        ("len", ctypes.c_int64),
+        ("data_pointer", ctypes.c_int64),
+        ("passes", ctypes.c_double),
+        ("max", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("total_p", ctypes.c_double),
+        ("n_nodes", ctypes.c_int64),
+        ("tree_size", ctypes.c_int64),
     ]
 
 
@@ -144,6 +175,19 @@ def lib() -> ctypes.CDLL:
     L.qc_actor_load.argtypes = [vp, P(QcDqnLayer)]
     L.qc_actor_noise_len.argtypes = [vp]
     L.qc_actor_act.argtypes = [vp, i64, i64, vp, i32, vp, d, u64, vp, vp, vp]
+    L.qc_replay_create.argtypes = [P(QcReplayParams), ctypes.c_int, P(vp)]
+    L.qc_replay_destroy.argtypes = [vp]
+    L.qc_replay_destroy.restype = None
+    L.qc_replay_last_error.argtypes = [vp]
+    L.qc_replay_last_error.restype = ctypes.c_char_p
+    L.qc_replay_set_stream.argtypes = [vp, vp]
+    L.qc_replay_store.argtypes = [vp, i64, vp, vp]
+    L.qc_replay_store_xp.argtypes = [vp, i64, vp, vp, vp, i32, vp, vp]
+    L.qc_replay_sample.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.qc_replay_update.argtypes = [vp, i32, vp, vp]
+    L.qc_replay_rebuild.argtypes = [vp]
+    L.qc_replay_stats.argtypes = [vp, P(QcReplayStats)]
+    L.qc_replay_buffers.argtypes = [vp, P(vp), P(vp)]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int:   # default
@@ -155,6 +199,13 @@ def lib() -> ctypes.CDLL:
 def check_actor(rc: int, handle=None) -> int:
     if rc < 0:
         msg = lib().qc_actor_last_error(handle)
+        raise QCartError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def check_replay(rc: int, handle=None) -> int:
+    if rc < 0:
+        msg = lib().qc_replay_last_error(handle)
         raise QCartError(rc, msg.decode() if msg else "")
     return rc
 

@@ -265,6 +265,64 @@ int qc_actor_act(qc_actor* a, int64_t B, int64_t env_offset, const float* obs, i
                  const float* noise, double eps, uint64_t counter, int32_t* actions, float* q_out,
                  int32_t* random_out);
 
+/* ---------------------------------------------------------------------------------------------
+ * Prioritized experience replay on the device: the reference's SumTree + Memory
+ * (inverted harmonic oscillator/RL.py:234-475), fed by BatchedEnv without leaving HBM.
+ * Layout as the reference: tree float64 [n_nodes + capacity] heap-indexed, leaf of slot d at n_nodes + d;
+ * data float32 [capacity][row_len]. All pointers below are device pointers; calls are asynchronous on
+ * the memory's stream (qc_replay_stats synchronises). */
+typedef struct qc_replay qc_replay;
+
+typedef struct qc_replay_params {
+    int64_t capacity;             /* round(size_of_replay_memory * n_con * 100) (IHO/main_parallel.py:595) */
+    int32_t row_len;              /* data_size of one row: 2 * obs_len + 2 ('xp'), qc_record_row_len ('measurements') */
+    int32_t policy;               /* 0 'sequential', 1 'random' (the drivers: 'random', main_parallel.py:598) */
+    double passes_before_random;  /* 0.2 (main_parallel.py:598); SumTree.passes starts at minus this */
+    double alpha;                 /* 0.2  Memory.alpha (RL.py:372)                    */
+    double beta;                  /* 0.2  Memory.beta, initial (RL.py:373)            */
+    double beta_increment;        /* 0.001 per sample (RL.py:374)                     */
+    double abs_err_upper;         /* 1.0 (RL.py:375)                                  */
+    double epsilon_scale;         /* 1e-5: epsilon = 1e-5 * max (RL.py:442)           */
+    uint64_t seed;                /* Philox key: random-policy positions, sampling uniforms */
+} qc_replay_params;
+
+typedef struct qc_replay_stats_t {
+    int64_t len;                  /* len(memory) (RL.py:415-416)  */
+    int64_t data_pointer;
+    double passes;
+    double max;                   /* Memory.max                    */
+    double beta;                  /* Memory.beta after the last sample */
+    double total_p;               /* SumTree.total_p = tree[0]     */
+    int64_t n_nodes, tree_size;
+} qc_replay_stats_t;
+
+int qc_replay_create(const qc_replay_params* p, int device, qc_replay** out);
+void qc_replay_destroy(qc_replay* r);
+const char* qc_replay_last_error(const qc_replay* r);   /* r may be NULL: last create failure */
+int qc_replay_set_stream(qc_replay* r, void* stream);
+/* Memory.store for each row e < n with valid[e] != 0 (valid NULL = all), in index order (RL.py:417-420,
+ * SumTree.add :273-288): priority max (or abs_err_upper while max == 0); 'sequential' slots while
+ * passes < 1, then random slots (Philox); a slot hit twice in one call keeps the later row. */
+int qc_replay_store(qc_replay* r, int64_t n, const uint8_t* valid, const float* rows /*[n][row_len]*/);
+/* the same, assembling the 'xp' experience row np.hstack((last_data, data, [last_action], [reward]))
+ * (IHO/main_parallel.py:250-257) from its parts: last_obs/obs [n][obs_len] fp32, action [n] int32,
+ * reward [n] fp32; row_len must be 2 * obs_len + 2 */
+int qc_replay_store_xp(qc_replay* r, int64_t n, const uint8_t* valid, const float* last_obs, const float* obs,
+                       int32_t obs_len, const int32_t* action, const float* reward);
+/* Memory.obtain_sample(n) / compiled_sampling (RL.py:423-432, :449-469): beta += increment (max 1),
+ * stratified v_i = (i + u_i) * total / n with u [n] injected (NULL: Philox), tree_idx [n] int32 leaf
+ * indices, is_weights [n] fp32 = (p / (total / len))^-beta, transitions [n][row_len] fp32 (NULL: skip the
+ * gather). Requires len >= 1 (the reference returns nothing while len < n). */
+int qc_replay_sample(qc_replay* r, int32_t n, const double* u, float* transitions, int32_t* tree_idx,
+                     float* is_weights);
+/* Memory.batch_update (RL.py:438-446, :471-475): abs_errors [n] fp32 (the per-sample losses) */
+int qc_replay_update(qc_replay* r, int32_t n, const int32_t* tree_idx, const float* abs_errors);
+/* Memory.clean / recalculate_structure (RL.py:312-331, :421-422): every parent recomputed */
+int qc_replay_rebuild(qc_replay* r);
+int qc_replay_stats(qc_replay* r, qc_replay_stats_t* out);
+/* device pointers of the tree and the row storage (introspection, tests) */
+int qc_replay_buffers(const qc_replay* r, const double** tree, const float** data);
+
 #ifdef __cplusplus
 }
 #endif

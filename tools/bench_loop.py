@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """End-to-end actor loop on one GPU (SURVEY §8f rank 1 measured in place): BatchedEnv (IHO N = 512) +
 DQNActor (direct_DQN, random-initialised weights of the reference architecture) for K control steps:
-act -> step (80 physics steps) -> experience rows, with auto-reset of finished episodes.
-Prints one JSON line: RL steps/s (decisions), env-steps/s and the actor's share of the loop.
+act -> step (80 physics steps) -> experience rows stored in the device prioritized replay (the drivers'
+capacity 7000 x 18 x 100 = 12.6 M rows, qc_replay_store_xp) -> one sample(512) + batch_update, the
+trainer's per-step memory traffic (RL.py:172, :224), with auto-reset of finished episodes.
+Prints one JSON line: RL steps/s (decisions), env-steps/s and the actor's / replay's share of the loop.
 usage: python tools/bench_loop.py [--batch B] [--steps K]"""
 import argparse
 import json
@@ -17,6 +19,7 @@ import torch  # noqa: E402
 from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
 from deepreinforcementlearningcontrolofquantumcartpoles_amd.actor import DQNActor, random_direct_dqn  # noqa: E402
 from deepreinforcementlearningcontrolofquantumcartpoles_amd.env import BatchedEnv  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.replay import PrioritizedReplay  # noqa: E402
 
 
 def main():
@@ -24,21 +27,24 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--capacity", type=int, default=7000 * 18 * 100)   # IHO/arguments.py:80, main_parallel.py:595
     args = ap.parse_args()
     B = args.batch
     ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)
     env = BatchedEnv(ph, B, 0, seed=1)
     actor = DQNActor({k: v.cuda() for k, v in random_direct_dqn(seed=1).items()}, max_batch=B, seed=2)
+    mem = PrioritizedReplay(args.capacity, 2 * 5 + 2, "random", 0.2, device=0, seed=3)
     obs = env.reset()
     steps_done = 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    actor_ms = 0.0
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    actor_ms = replay_ms = 0.0
     rows = 0
     for it in range(args.warmup + args.steps):
         if it == args.warmup:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            actor_ms = 0.0
+            actor_ms = replay_ms = 0.0
             rows = 0
         e0.record()
         a = actor.act(obs, eps=DQNActor.eps_threshold(steps_done))
@@ -46,9 +52,15 @@ def main():
         steps_done += B
         obs, reward, done, info = env.step(a)
         rows += int(info["valid"].sum())
-        BatchedEnv.experience(info["last_obs"], obs, a, reward)
-        e1.synchronize()
+        r0.record()
+        mem.store_xp(info["last_obs"], obs, a, reward, info["valid"])
+        smp = mem.obtain_sample(512) if it > 0 else None
+        if smp is not None:
+            mem.batch_update(smp[0], torch.rand(512, device="cuda"))
+        r1.record()
+        r1.synchronize()
         actor_ms += e0.elapsed_time(e1)
+        replay_ms += r0.elapsed_time(r1)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     K = args.steps
@@ -56,6 +68,8 @@ def main():
                       "value": B * K / dt, "unit": "decisions/s", "env_steps_per_s": B * K * ph.control_interval / dt,
                       "batch": B, "control_steps": K, "ms_per_control_step": dt / K * 1e3,
                       "actor_ms_per_control_step": actor_ms / K, "actor_share": actor_ms / (dt * 1e3),
+                      "replay_ms_per_control_step": replay_ms / K, "replay_share": replay_ms / (dt * 1e3),
+                      "replay_len": len(mem),
                       "experience_rows_per_s": rows / dt,
                       "data": "synthetic: |0> resets, random-initialised direct_DQN weights"}), flush=True)
 

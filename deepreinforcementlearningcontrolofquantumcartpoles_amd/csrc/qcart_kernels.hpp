@@ -215,6 +215,15 @@ __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
     for (int i = 0; i < NV; ++i) v[i] = readlane_d(v[i], 63);
 }
 
+// the step kernel's reductions. (Measured and rejected: the sum on the matrix core, two
+// v_mfma_f64_16x16x4_f64 against an all-ones B per value — 26.3 -> 28.2 ms per metric launch: on
+// MI355X the FP64 MFMA shares the FP64 pipe's rate, so each MFMA costs 16 FMA issues, and its
+// latency sits on the step's critical path.)
+template <int NV>
+__device__ __forceinline__ void step_sum(double (&v)[NV]) {
+    wave_sum<NV>(v);
+}
+
 // ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
 template <int FAM>
 struct Fam;
@@ -965,7 +974,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             const int r = base + j;
             if (r >= a.win_lo && r < a.win_hi) s[1] += (double)(psi[j].re * psi[j].re + psi[j].im * psi[j].im);
         }
-        wave_sum<2>(s);
+        step_sum<2>(s);
         xbar = (RT)(a.w * s[0]);                                  // x_expct (IHO:197-203, QO:230-236)
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
@@ -1117,7 +1126,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 sm[0] = dot_acc(sm[0], j == 0, psi[j], xYp[j]);
                 sm[1] = dot_acc(sm[1], j == 0, Ym[j], xYm[j]);
             }
-            wave_sum<2>(sm);
+            step_sum<2>(sm);
             yp = a.w * sm[0];
             ym = a.w * sm[1];
             const RT ymr = (RT)ym;
@@ -1160,7 +1169,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 d2[0] = dot_acc(dot_acc(d2[0], j == 0, psi[j], xrp[j]), false, rp[j], xYp[j]);
                 d2[1] = dot_acc(d2[1], j == 0, rp[j], xrp[j]);
             }
-            wave_sum<2>(d2);
+            step_sum<2>(d2);
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
@@ -1212,7 +1221,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
                 for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
             }
-            wave_sum<2>(s);
+            step_sum<2>(s);
             // 1/sqrt(s0): hardware estimate + two Newton steps (full fp64 precision)
             double scale = __builtin_amdgcn_rsq(s[0]);
             scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
@@ -1232,7 +1241,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             if constexpr (FAM == 2) {
                 if (win_on && term < 0) {
                     double sw[1] = {pwin};
-                    wave_sum<1>(sw);
+                    step_sum<1>(sw);
                     if (1.0 - a.h * (sw[0] * scale) * scale > 0.5) term = k + 1;
                 }
             }

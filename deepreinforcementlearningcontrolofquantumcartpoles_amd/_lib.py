@@ -32,6 +32,8 @@ EXPORTS = (
     "qc_scan_levels",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
+    "qc_mactor_create", "qc_mactor_destroy", "qc_mactor_last_error", "qc_mactor_set_stream", "qc_mactor_noise_len",
+    "qc_mactor_flat_len", "qc_mactor_load", "qc_mactor_act",
     "qc_replay_create", "qc_replay_destroy", "qc_replay_last_error", "qc_replay_set_stream", "qc_replay_store",
     "qc_replay_store_xp", "qc_replay_sample", "qc_replay_update", "qc_replay_rebuild", "qc_replay_stats",
     "qc_replay_buffers",
@@ -67,6 +69,16 @@ class QcDqnParams(ctypes.Structure):
         ("n_actions", ctypes.c_int32),
         ("max_batch", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
+    ]
+
+
+class QcMdqnParams(ctypes.Structure):
+    _fields_ = [
+        ("read_length", ctypes.c_int32),
+        ("n_actions", ctypes.c_int32),
+        ("max_batch", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("chunk", ctypes.c_int32),
     ]
 
 
@@ -175,6 +187,16 @@ def lib() -> ctypes.CDLL:
     L.qc_actor_load.argtypes = [vp, P(QcDqnLayer)]
     L.qc_actor_noise_len.argtypes = [vp]
     L.qc_actor_act.argtypes = [vp, i64, i64, vp, i32, vp, d, u64, vp, vp, vp]
+    L.qc_mactor_create.argtypes = [P(QcMdqnParams), ctypes.c_int, P(vp)]
+    L.qc_mactor_destroy.argtypes = [vp]
+    L.qc_mactor_destroy.restype = None
+    L.qc_mactor_last_error.argtypes = [vp]
+    L.qc_mactor_last_error.restype = ctypes.c_char_p
+    L.qc_mactor_set_stream.argtypes = [vp, vp]
+    L.qc_mactor_noise_len.argtypes = [vp]
+    L.qc_mactor_flat_len.argtypes = [vp]
+    L.qc_mactor_load.argtypes = [vp, P(QcDqnLayer)]
+    L.qc_mactor_act.argtypes = [vp, i64, i64, vp, i32, vp, d, u64, vp, vp, vp]
     L.qc_replay_create.argtypes = [P(QcReplayParams), ctypes.c_int, P(vp)]
     L.qc_replay_destroy.argtypes = [vp]
     L.qc_replay_destroy.restype = None
@@ -199,6 +221,13 @@ def lib() -> ctypes.CDLL:
 def check_actor(rc: int, handle=None) -> int:
     if rc < 0:
         msg = lib().qc_actor_last_error(handle)
+        raise QCartError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def check_mactor(rc: int, handle=None) -> int:
+    if rc < 0:
+        msg = lib().qc_mactor_last_error(handle)
         raise QCartError(rc, msg.decode() if msg else "")
     return rc
 

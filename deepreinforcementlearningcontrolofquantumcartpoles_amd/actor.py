@@ -167,3 +167,150 @@ def random_direct_dqn(data_length: int = 5, n_actions: int = 21, noisy_layers: i
     p.update(noisy("fc41", 256, n_actions) if noisy_layers >= 1 else linear("fc41", 256, n_actions))
     p.update(linear("fc42", 128, 1))
     return {k: v.to(device=device, dtype=torch.float32) for k, v in p.items()}
+
+
+M_LAYERS = ("conv1", "conv2", "conv3", "fc1", "fc21", "fc31")
+M_CONV = ((2, 32, 13, 5), (32, 64, 11, 4), (64, 64, 9, 4))   # (in, out, kernel, stride), RL.py:36-45
+
+
+def conv_out(n: int, k: int, s: int) -> int:
+    """calculate_next_layer_dim (IHO/RL.py:49-50)."""
+    return (n - (k - 1) + (s - 1)) // s
+
+
+def measurement_flat_len(read_length: int) -> int:
+    n = read_length
+    for _, _, k, s in M_CONV:
+        n = conv_out(n, k, s)
+    return 64 * n
+
+
+class MeasurementActor:
+    """Device-side action selection for B envs with a reference DQN_measurement's parameters (the
+    'measurements' input, IHO/RL.py:29-78): obs = MeasurementRecord.hist [B, 2, read_length]."""
+
+    def __init__(self, params: Mapping[str, torch.Tensor], read_length: int = 5760, n_actions: int = 21,
+                 max_batch: int = 65536, device: int | str | torch.device = 0, seed: int = 0, chunk: int = 0):
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("MeasurementActor runs on a HIP device only (no CPU fallback)")
+        self.read_length, self.n_actions, self.max_batch = int(read_length), int(n_actions), int(max_batch)
+        p = L.QcMdqnParams()
+        p.read_length, p.n_actions, p.max_batch, p.seed, p.chunk = (self.read_length, self.n_actions,
+                                                                     self.max_batch, int(seed), int(chunk))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check_mactor(L.lib().qc_mactor_create(ctypes.byref(p), self.device.index or 0, ctypes.byref(h)), None)
+        self._h = h
+        self.noise_len = int(L.lib().qc_mactor_noise_len(h))
+        self.flat_len = int(L.lib().qc_mactor_flat_len(h))
+        self.counter = 0
+        self._keep = []
+        self.load(params)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().qc_mactor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        L.check_mactor(L.lib().qc_mactor_set_stream(self._h, ctypes.c_void_p(s)), self._h)
+
+    def load(self, params: Mapping[str, torch.Tensor]):
+        layers = (L.QcDqnLayer * 6)()
+        keep = []
+        shapes = [(o, i * k) for i, o, k, _ in M_CONV] + [(256, self.flat_len), (256, 256), (self.n_actions, 256)]
+        for j, name in enumerate(M_LAYERS):
+            if j < 4:
+                w = params[f"{name}.weight"].detach().to(device=self.device, dtype=torch.float32)
+                w = w.reshape(w.shape[0], -1).contiguous()
+                b = params[f"{name}.bias"].detach().to(device=self.device, dtype=torch.float32).contiguous()
+                g = sw = sb = None
+            else:
+                w, b, g, sw, sb = _layer_tensors(params, name, self.device)
+            if tuple(w.shape) != shapes[j]:
+                raise ValueError(f"{name}: weight shape {tuple(w.shape)} != {shapes[j]}")
+            keep += [w, b, g, sw, sb]
+            layers[j].weight, layers[j].bias = w.data_ptr(), b.data_ptr()
+            layers[j].weight_norm = g.data_ptr() if g is not None else None
+            layers[j].sigma_w = sw.data_ptr() if sw is not None else None
+            layers[j].sigma_b = sb.data_ptr() if sb is not None else None
+        with torch.cuda.device(self.device):
+            self._bind_stream()
+            L.check_mactor(L.lib().qc_mactor_load(self._h, layers), self._h)
+        self._keep = keep
+
+    def act(self, obs: torch.Tensor, eps: float = 0.0, noisy: bool = True, counter: Optional[int] = None,
+            noise: Optional[torch.Tensor] = None, env_offset: int = 0, want_q: bool = False,
+            want_random: bool = False):
+        """As DQNActor.act for obs [B, 2, read_length] (the measurement record)."""
+        if obs.dim() != 3 or obs.shape[1] != 2 or obs.shape[2] != self.read_length:
+            raise ValueError(f"obs must be [B, 2, {self.read_length}]")
+        B = obs.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f"B = {B} exceeds max_batch = {self.max_batch}")
+        obs = obs.to(device=self.device, dtype=torch.float32).contiguous()
+        if counter is None:
+            counter = self.counter
+            self.counter += 1
+        nz = None
+        if noise is not None:
+            if tuple(noise.shape) != (B, self.noise_len):
+                raise ValueError(f"noise must be [B, {self.noise_len}]")
+            nz = noise.to(device=self.device, dtype=torch.float32).contiguous()
+        actions = torch.empty(B, dtype=torch.int32, device=self.device)
+        q = torch.empty((B, self.n_actions), dtype=torch.float32, device=self.device) if want_q else None
+        rnd = torch.empty(B, dtype=torch.int32, device=self.device) if want_random else None
+        vp = ctypes.c_void_p
+        with torch.cuda.device(self.device):
+            self._bind_stream()
+            L.check_mactor(L.lib().qc_mactor_act(
+                self._h, B, int(env_offset), vp(obs.data_ptr()), 1 if noisy else 0,
+                vp(nz.data_ptr()) if nz is not None else None, float(eps), int(counter),
+                vp(actions.data_ptr()), vp(q.data_ptr()) if q is not None else None,
+                vp(rnd.data_ptr()) if rnd is not None else None), self._h)
+        if want_q or want_random:
+            return actions, {"q": q, "random": rnd}
+        return actions
+
+
+def random_dqn_measurement(read_length: int = 5760, n_actions: int = 21, seed: int = 0,
+                           device: str | torch.device = "cpu") -> dict:
+    """Random-initialised parameters of the reference DQN_measurement (RL.py:29-78) as a state_dict:
+    PyTorch's default Conv1d / Linear initialisers (conv biases zeroed, RL.py:46-48), FactorizedNoisy as
+    in random_direct_dqn, and the unused mean branch fc22 / fc32. Synthetic weights for tests / benches."""
+    g = torch.Generator().manual_seed(seed)
+
+    def uni(shape, bound):
+        return (torch.rand(shape, generator=g) * 2 - 1) * bound
+
+    p = {}
+    for j, (ci, co, k, _) in enumerate(M_CONV):
+        bound = 1.0 / math.sqrt(ci * k)
+        p[f"conv{j + 1}.weight"] = uni((co, ci, k), bound)
+        p[f"conv{j + 1}.bias"] = torch.zeros(co)
+    flat = measurement_flat_len(read_length)
+    p["fc1.weight"] = uni((256, flat), 1.0 / math.sqrt(flat))
+    p["fc1.bias"] = uni((256,), 1.0 / math.sqrt(flat))
+
+    def noisy(name, i, o):
+        s = 0.5 / math.sqrt(i)
+        return {f"{name}.u_w": uni((o, i), math.sqrt(6.0 / i)), f"{name}.sigma_w": torch.full((o, i), s),
+                f"{name}.u_b": torch.zeros(o), f"{name}.sigma_b": torch.full((o,), s)}
+
+    def linear(name, i, o):
+        w = uni((o, i), 1.0 / math.sqrt(i))
+        return {f"{name}.weight": w, f"{name}.bias": uni((o,), 1.0 / math.sqrt(i)), f"{name}.weight_norm": w.norm()}
+
+    p.update(noisy("fc21", 256, 256))
+    p.update(noisy("fc31", 256, n_actions))
+    p.update(linear("fc22", 256, 128))
+    p.update(linear("fc32", 128, 1))
+    return {k: v.to(device=device, dtype=torch.float32) for k, v in p.items()}

@@ -55,6 +55,10 @@ struct ActArgs {
     int32_t* actions;
     float* q_out;
     int32_t* random_out;
+    // measurement network (DQN_measurement): the 256-wide fc1 output, feature-major [256][h_ld], enters
+    // as H2; fc1 / fc2 of direct_DQN are skipped and L[2] / L[3] hold fc21 / fc31
+    const float* h_in;
+    int64_t h_ld;
 };
 
 // acc += A_frag(W) . X  over `steps` k-steps (X: LDS [k][32]; lane reads X[2s + (lane>>5)][lane&31]).
@@ -109,6 +113,21 @@ __global__ __launch_bounds__(kThreads) void k_actor_act(const ActArgs a) {
     const int64_t eg = e0 + env;          // this lane's env (D column)
     const bool env_ok = eg < a.B;
 
+    float* H2 = RB;
+    float* H2e = RB + kH2 * kE;
+    const bool n31 = a.noisy && a.L[2].s != nullptr;
+    if (a.h_in) {
+        // DQN_measurement: relu(fc1(x)) from HBM (coalesced 32-env rows) -> H2, eps_in(fc21) o H2
+        for (int i = tid; i < kH2 * kE; i += kThreads) {
+            const int k = i / kE, e = i % kE;
+            const bool ok = e0 + e < a.B;
+            const float h = ok ? a.h_in[(int64_t)k * a.h_ld + e0 + e] : 0.f;
+            H2[i] = h;
+            if (n31) H2e[i] = ok ? h * noise_at(a, k, e0 + e) : 0.f;
+        }
+        __syncthreads();
+        goto fc31;
+    }
     // ---- input: the fp32 network input (IHO/main_parallel.py:131,241) -> X0[k][env]
     for (int i = tid; i < a.in_pad * kE; i += kThreads) {
         const int k = i / kE, e = i % kE;
@@ -129,9 +148,6 @@ __global__ __launch_bounds__(kThreads) void k_actor_act(const ActArgs a) {
     __syncthreads();
 
     // ---- fc2: 256 outputs = 8 tiles, 2 per wave; ReLU; also eps_in(fc31) o H2 for the noisy GEMM
-    float* H2 = RB;
-    float* H2e = RB + kH2 * kE;
-    const bool n31 = a.noisy && a.L[2].s != nullptr;
     for (int t = wave; t < tiles(kH2); t += 4) {
         f32x16 acc = {};
         gemm_tile(acc, a.L[1].u + (size_t)t * ksteps(kH1) * 64, RA, ksteps(kH1), lane);
@@ -146,6 +162,7 @@ __global__ __launch_bounds__(kThreads) void k_actor_act(const ActArgs a) {
     __syncthreads();
 
     // ---- fc31 (noisy or weight-normalised): 8 tiles, 2 per wave; ReLU; eps_in(fc41) o H3
+fc31:
     float* H3 = RA;
     float* H3e = RA + kH3 * kE;
     const bool n41 = a.noisy && a.L[3].s != nullptr;
@@ -265,6 +282,150 @@ __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float
     }
     if (bias_pad)
         for (int i = threadIdx.x; i < T * 32; i += 1024) bias_pad[i] = (i < O && bias) ? bias[i] : 0.f;
+}
+
+// ---- DQN_measurement (IHO/RL.py:29-78): Conv1d stack as implicit GEMMs on f32 MFMA ----------------
+// Y[b][co][t] = relu(bias[co] + sum_{ci, j} W[co][ci][j] X[b][ci][S t + j]): M = co (MT tiles of 32),
+// N = (env, position) flattened (32 columns per wave), K = ci * KS in pairs (k = ci * KS + j, the
+// PyTorch weight order). A = weight fragments (k_actor_prep order), B = the input gathered per lane
+// from HBM / L2 (column base X[b] + S t; row offset ci * Tin + j, wave-uniform per k-step half).
+// Loads run a batch of kQ steps ahead of the MFMAs. Output: env-major [b][co][t] (layers 1, 2) or
+// feature-major [co * Tout + t][y_ld] at env column y_off + b (layer 3: fc1's B operand, coalesced).
+constexpr int kQ = 8;
+constexpr int kNT = 2;   // column tiles per wave: every weight fragment feeds kNT MFMAs
+template <int CI, int KS, int S, int MT>
+__global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int Tin, const float* __restrict__ Wf,
+                                               const float* __restrict__ bias, float* __restrict__ Y, int Tout,
+                                               int64_t n_total, int feat_major, int64_t y_ld, int64_t y_off) {
+    constexpr int K = CI * KS, STEPS = (K + 1) / 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int hi = lane >> 5;
+    bool col_ok[kNT];
+    int64_t bb[kNT];
+    int tt[kNT];
+    const float* xc[kNT];
+#pragma unroll
+    for (int c = 0; c < kNT; ++c) {
+        const int64_t n = (((int64_t)blockIdx.x * 4 + wave) * kNT + c) * 32 + (lane & 31);
+        col_ok[c] = n < n_total;
+        bb[c] = col_ok[c] ? n / Tout : 0;
+        tt[c] = col_ok[c] ? (int)(n - bb[c] * Tout) : 0;
+        xc[c] = X + bb[c] * (int64_t)CI * Tin + (int64_t)S * tt[c];
+    }
+    auto xoff = [&](int s) -> int {   // row offset of k = 2 s + hi: ci * Tin + j
+        const int k = 2 * s + hi;
+        return (k / KS) * Tin + (k % KS);
+    };
+    f32x16 acc[MT][kNT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int c = 0; c < kNT; ++c) acc[m][c] = f32x16{};
+    const float* wl = Wf + lane;
+    constexpr int FULL = STEPS / kQ * kQ;
+    float xb[kQ][kNT], wb[kQ][MT];
+    auto fetch = [&](int s, float (&x)[kNT], float (&w)[MT]) {
+        const bool ok = s < STEPS && 2 * s + hi < K;
+        const int o = ok ? xoff(s) : 0;
+#pragma unroll
+        for (int c = 0; c < kNT; ++c) x[c] = (ok && col_ok[c]) ? xc[c][o] : 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) w[m] = s < STEPS ? wl[((int64_t)m * STEPS + s) * 64] : 0.f;
+    };
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) fetch(u, xb[u], wb[u]);
+    for (int s = 0; s < FULL; s += kQ) {
+        float xn[kQ][kNT], wn[kQ][MT];
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) fetch(s + kQ + u, xn[u], wn[u]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kQ; ++u)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int c = 0; c < kNT; ++c)
+                    acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u][c], acc[m][c], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) {
+#pragma unroll
+            for (int c = 0; c < kNT; ++c) xb[u][c] = xn[u][c];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) wb[u][m] = wn[u][m];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kQ; ++u)
+        if (FULL + u < STEPS)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int c = 0; c < kNT; ++c)
+                    acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u][c], acc[m][c], 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < kNT; ++c) {
+        if (!col_ok[c]) continue;
+        const int64_t b = bb[c];
+        const int t = tt[c];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = m * 32 + drow(r, lane);
+                const float v = fmaxf(acc[m][c][r] + bias[co], 0.f);
+                if (feat_major) Y[((int64_t)co * Tout + t) * y_ld + y_off + b] = v;
+                else Y[(b * (MT * 32) + co) * (int64_t)Tout + t] = v;
+            }
+    }
+}
+
+// fc1 (nn.Linear K -> 256) + ReLU for 32 envs per wave: B = the feature-major conv output
+// X[k][x_ld] (one coalesced 128-B row per k-step half), 8 row tiles share each B load.
+__global__ __launch_bounds__(256) void k_mfc(const float* __restrict__ X, int64_t x_ld, int K,
+                                             const float* __restrict__ Wf, const float* __restrict__ bias,
+                                             float* __restrict__ H, int64_t B) {
+    constexpr int MT = 8;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t e = ((int64_t)blockIdx.x * 4 + wave) * 32 + (lane & 31);
+    const bool ok = e < B;
+    const int steps = (K + 1) / 2, hi = lane >> 5;
+    const float* xc = X + (ok ? e : 0);
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x16{};
+    const float* wl = Wf + lane;
+    constexpr int Q = 4;
+    int s = 0;
+    for (; s + Q <= steps; s += Q) {
+        float xb[Q], wb[Q][MT];
+#pragma unroll
+        for (int u = 0; u < Q; ++u) {
+            const int k = 2 * (s + u) + hi;
+            xb[u] = (ok && k < K) ? xc[(int64_t)k * x_ld] : 0.f;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) wb[u][m] = wl[((int64_t)m * steps + s + u) * 64];
+        }
+#pragma unroll
+        for (int u = 0; u < Q; ++u)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u], acc[m], 0, 0, 0);
+    }
+    for (; s < steps; ++s) {
+        const int k = 2 * s + hi;
+        const float xv = (ok && k < K) ? xc[(int64_t)k * x_ld] : 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[((int64_t)m * steps + s) * 64], xv, acc[m], 0, 0, 0);
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = m * 32 + drow(r, lane);
+            H[(int64_t)o * x_ld + e] = fmaxf(acc[m][r] + bias[o], 0.f);   // feature-major [256][ld]
+        }
 }
 
 }  // namespace actor
@@ -468,6 +629,226 @@ int qc_actor_act(qc_actor* a, int64_t B, int64_t env_offset, const float* obs, i
                        (2 * kH1 * kE + 16 * 64) * sizeof(float), a->stream, k);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(a, e, "actor launch");
+    return QC_OK;
+}
+
+}  // extern "C"
+
+// ---- the measurement-input actor (DQN_measurement, IHO/RL.py:29-78) --------------------------------
+struct qc_mactor {
+    qc_mdqn_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int T1 = 0, T2 = 0, T3 = 0, flat = 0, chunk = 0, noise_len = 0;
+    bool loaded = false, has_s21 = false, has_s31 = false;
+    float* d_w = nullptr;
+    size_t off_w[6]{}, off_b[6]{}, off_s[6]{}, off_sb[6]{};
+    float *d_y1 = nullptr, *d_y2 = nullptr, *d_y3 = nullptr, *d_h1 = nullptr, *d_noise = nullptr;
+};
+
+namespace {
+std::string g_mactor_err;
+// layer shapes: conv1 (32, 2, 13, /5), conv2 (64, 32, 11, /4), conv3 (64, 64, 9, /4) (RL.py:36-45)
+constexpr int kC1 = 32, kC2 = 64, kC3 = 64;
+int conv_out(int n, int k, int s) { return (n - (k - 1) + (s - 1)) / s; }   // calculate_next_layer_dim (RL.py:49-50)
+}  // namespace
+
+extern "C" {
+
+int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out) {
+    if (!out || !p) return QC_EINVAL;
+    *out = nullptr;
+    auto fail = [](const char* m, int rc) {
+        std::lock_guard<std::mutex> lk(g_actor_mu);
+        g_mactor_err = m;
+        return rc;
+    };
+    if (p->n_actions < 1 || p->n_actions > 32) return fail("n_actions must be in [1, 32]", QC_EINVAL);
+    if (p->max_batch < 1) return fail("max_batch must be >= 1", QC_EINVAL);
+    qc_mactor* a = new qc_mactor();
+    a->p = *p;
+    a->device = device;
+    a->T1 = conv_out(p->read_length, 13, 5);
+    a->T2 = conv_out(a->T1, 11, 4);
+    a->T3 = conv_out(a->T2, 9, 4);
+    if (p->read_length < 1 || a->T3 < 1) {
+        delete a;
+        return fail("read_length too short for the three convolutions", QC_EINVAL);
+    }
+    a->flat = kC3 * a->T3;
+    a->noise_len = 2 * kH2 + kH3 + p->n_actions;
+    a->chunk = (int)std::min<int64_t>(p->max_batch, p->chunk > 0 ? p->chunk : 1024);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        delete a;
+        return fail("no HIP device available (the actor has no CPU fallback)", QC_EHIP);
+    }
+    if (device < 0 || device >= ndev) {
+        delete a;
+        return fail("device index out of range", QC_EINVAL);
+    }
+    const int O[6] = {kC1, kC2, kC3, kH2, kH3, p->n_actions};
+    const int K[6] = {2 * 13, kC1 * 11, kC2 * 9, a->flat, kH2, kH3};
+    size_t off = 0;
+    for (int l = 0; l < 6; ++l) {
+        const size_t fr = (size_t)tiles(O[l]) * ksteps(K[l]) * 64, bp = (size_t)tiles(O[l]) * 32;
+        a->off_w[l] = off; off += fr;
+        a->off_b[l] = off; off += bp;
+        if (l >= 4) {
+            a->off_s[l] = off; off += fr;
+            a->off_sb[l] = off; off += bp;
+        }
+    }
+    Dev g(device);
+    const size_t mb = (size_t)p->max_batch, ch = (size_t)a->chunk;
+    hipError_t e = hipMalloc(&a->d_w, off * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(a->d_w, 0, off * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_y1, ch * kC1 * a->T1 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_y2, ch * kC2 * a->T2 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_y3, (size_t)a->flat * mb * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_h1, (size_t)kH2 * mb * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_noise, (size_t)a->noise_len * mb * sizeof(float));
+    if (e == hipSuccess &&
+        hipFuncSetAttribute((const void*)k_actor_act, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (2 * kH1 * kE + 16 * 64) * (int)sizeof(float)) != hipSuccess)
+        e = hipErrorInvalidValue;
+    if (e != hipSuccess) {
+        qc_mactor_destroy(a);
+        return fail("device allocation failed", QC_ENOMEM);
+    }
+    *out = a;
+    return QC_OK;
+}
+
+void qc_mactor_destroy(qc_mactor* a) {
+    if (!a) return;
+    {
+        Dev g(a->device);
+        (void)hipDeviceSynchronize();
+        for (float* q : {a->d_w, a->d_y1, a->d_y2, a->d_y3, a->d_h1, a->d_noise})
+            if (q) (void)hipFree(q);
+    }
+    delete a;
+}
+
+const char* qc_mactor_last_error(const qc_mactor* a) {
+    if (a) return a->err.c_str();
+    std::lock_guard<std::mutex> lk(g_actor_mu);
+    return g_mactor_err.c_str();
+}
+
+int qc_mactor_set_stream(qc_mactor* a, void* stream) {
+    if (!a) return QC_EINVAL;
+    a->stream = (hipStream_t)stream;
+    return QC_OK;
+}
+
+int qc_mactor_noise_len(const qc_mactor* a) { return a ? a->noise_len : QC_EINVAL; }
+int qc_mactor_flat_len(const qc_mactor* a) { return a ? a->flat : QC_EINVAL; }
+
+int qc_mactor_load(qc_mactor* a, const qc_dqn_layer layers[6]) {
+    if (!a || !layers) return QC_EINVAL;
+    const int O[6] = {kC1, kC2, kC3, kH2, kH3, a->p.n_actions};
+    const int K[6] = {2 * 13, kC1 * 11, kC2 * 9, a->flat, kH2, kH3};
+    for (int l = 0; l < 6; ++l) {
+        const qc_dqn_layer& L = layers[l];
+        if (!L.weight || !L.bias) { a->err = "layer " + std::to_string(l) + ": weight and bias are required"; return QC_EINVAL; }
+        if (l < 4 && (L.sigma_w || L.weight_norm)) {
+            a->err = "conv1..3 and fc1 are plain Conv1d / Linear layers (no weight_norm, no sigma)";
+            return QC_EINVAL;
+        }
+        if ((L.sigma_w == nullptr) != (L.sigma_b == nullptr)) { a->err = "sigma_w and sigma_b go together"; return QC_EINVAL; }
+        if (l >= 4 && !L.sigma_w && !L.weight_norm) { a->err = "fc21 / fc31: FactorizedNoisy or Linear_weight_normalize"; return QC_EINVAL; }
+    }
+    Dev g(a->device);
+    float* w = a->d_w;
+    for (int l = 0; l < 6; ++l) {
+        const qc_dqn_layer& L = layers[l];
+        const int Kp = (K[l] + 1) & ~1;
+        hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.weight, L.weight_norm, O[l], K[l], Kp,
+                           w + a->off_w[l], L.bias, w + a->off_b[l]);
+        if (l >= 4 && L.sigma_w)
+            hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.sigma_w, (const float*)nullptr, O[l],
+                               K[l], Kp, w + a->off_s[l], L.sigma_b, w + a->off_sb[l]);
+    }
+    a->has_s21 = layers[4].sigma_w != nullptr;
+    a->has_s31 = layers[5].sigma_w != nullptr;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        a->err = std::string("measurement actor weight preparation: ") + hipGetErrorString(e);
+        return QC_EHIP;
+    }
+    a->loaded = true;
+    return QC_OK;
+}
+
+int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs, int32_t noisy, const float* noise,
+                  double eps, uint64_t counter, int32_t* actions, float* q_out, int32_t* random_out) {
+    if (!a) return QC_EINVAL;
+    if (!a->loaded) { a->err = "qc_mactor_load has not been called"; return QC_EINVAL; }
+    if (B < 0 || B > a->p.max_batch) { a->err = "B must be in [0, max_batch]"; return QC_EINVAL; }
+    if (B == 0) return QC_OK;
+    if (!obs || !actions) { a->err = "obs and actions are required"; return QC_EINVAL; }
+    Dev g(a->device);
+    const int L = a->p.read_length;
+    const float* w = a->d_w;
+    const int64_t ld = a->p.max_batch;
+    for (int64_t c0 = 0; c0 < B; c0 += a->chunk) {   // conv stack per env chunk (its activations stay in L2 / MALL)
+        const int64_t nb = std::min<int64_t>(a->chunk, B - c0);
+        const int64_t n1 = nb * a->T1, n2 = nb * a->T2, n3 = nb * a->T3;
+        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1>), dim3((unsigned)((n1 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
+                           obs + c0 * 2 * L, L, w + a->off_w[0], w + a->off_b[0], a->d_y1, a->T1, n1, 0, (int64_t)0,
+                           (int64_t)0);
+        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2>), dim3((unsigned)((n2 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
+                           a->d_y1, a->T1, w + a->off_w[1], w + a->off_b[1], a->d_y2, a->T2, n2, 0, (int64_t)0,
+                           (int64_t)0);
+        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2>), dim3((unsigned)((n3 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
+                           a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3, a->T3, n3, 1, ld, c0);
+    }
+    hipLaunchKernelGGL(k_mfc, dim3((unsigned)((B + 127) / 128)), dim3(256), 0, a->stream, a->d_y3, ld, a->flat,
+                       w + a->off_w[3], w + a->off_b[3], a->d_h1, B);
+    const bool need_noise = noisy && (a->has_s21 || a->has_s31);
+    if (need_noise) {
+        if (noise) {
+            const int64_t n = B * a->noise_len;
+            hipLaunchKernelGGL(k_actor_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, a->stream, noise,
+                               a->d_noise, ld, B, a->noise_len);
+        } else {
+            hipLaunchKernelGGL(k_actor_noise, dim3((unsigned)((B + 255) / 256), (unsigned)((a->noise_len + 1) / 2)),
+                               dim3(256), 0, a->stream, a->d_noise, ld, B, a->noise_len, env_offset, a->p.seed, counter);
+        }
+    }
+    ActArgs k{};
+    k.L[2].u = w + a->off_w[4];
+    k.L[2].ub = w + a->off_b[4];
+    k.L[2].s = a->has_s21 ? w + a->off_s[4] : nullptr;
+    k.L[2].sb = a->has_s21 ? w + a->off_sb[4] : nullptr;
+    k.L[3].u = w + a->off_w[5];
+    k.L[3].ub = w + a->off_b[5];
+    k.L[3].s = a->has_s31 ? w + a->off_s[5] : nullptr;
+    k.L[3].sb = a->has_s31 ? w + a->off_sb[5] : nullptr;
+    k.n_act = a->p.n_actions;
+    k.B = B;
+    k.env_offset = env_offset;
+    k.noisy = need_noise ? 1 : 0;
+    k.noise = a->d_noise;
+    k.noise_ld = ld;
+    k.eps = (float)eps;
+    k.seed = a->p.seed;
+    k.counter = counter;
+    k.actions = actions;
+    k.q_out = q_out;
+    k.random_out = random_out;
+    k.h_in = a->d_h1;
+    k.h_ld = ld;
+    hipLaunchKernelGGL(k_actor_act, dim3((unsigned)((B + kE - 1) / kE)), dim3(kThreads),
+                       (2 * kH1 * kE + 16 * 64) * sizeof(float), a->stream, k);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        a->err = std::string("measurement actor launch: ") + hipGetErrorString(e);
+        return QC_EHIP;
+    }
     return QC_OK;
 }
 

@@ -265,6 +265,35 @@ int qc_actor_act(qc_actor* a, int64_t B, int64_t env_offset, const float* obs, i
                  const float* noise, double eps, uint64_t counter, int32_t* actions, float* q_out,
                  int32_t* random_out);
 
+/* The measurement-input actor (SURVEY §8f rank 1 for args.input == 'measurements'): DQN_measurement
+ * (inverted harmonic oscillator/RL.py:29-78) for B envs: conv1 Conv1d(2, 32, 13, stride 5), conv2
+ * Conv1d(32, 64, 11, 4), conv3 Conv1d(64, 64, 9, 4) with ReLU, flatten, fc1 Linear(64 T3, 256) + ReLU,
+ * fc21 FactorizedNoisy(256, 256) + ReLU, fc31 FactorizedNoisy(256, n_actions) -> argmax, epsilon-greedy.
+ * The convolutions run as implicit GEMMs on f32 MFMA over env chunks; the noise layout and the
+ * epsilon-greedy draw are qc_actor's (noise_len = 789 at 21 actions). */
+typedef struct qc_mdqn_params {
+    int32_t read_length;   /* network input length per channel (5760 IHO, 4320 HO; MeasurementRecord) */
+    int32_t n_actions;     /* 21 */
+    int64_t max_batch;
+    uint64_t seed;
+    int32_t chunk;         /* envs per convolution chunk (0: 1024) */
+} qc_mdqn_params;
+typedef struct qc_mactor qc_mactor;
+int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out);
+void qc_mactor_destroy(qc_mactor* a);
+const char* qc_mactor_last_error(const qc_mactor* a);
+int qc_mactor_set_stream(qc_mactor* a, void* stream);
+int qc_mactor_noise_len(const qc_mactor* a);
+int qc_mactor_flat_len(const qc_mactor* a);   /* 64 * T3, fc1's input length */
+/* layers[6] = conv1, conv2, conv3, fc1 (weight [out][in(*kernel)], bias; weight_norm = sigma = NULL),
+ * fc21, fc31 (FactorizedNoisy u_w/u_b/sigma_w/sigma_b, or Linear_weight_normalize) — the state_dict */
+int qc_mactor_load(qc_mactor* a, const qc_dqn_layer layers[6]);
+/* obs [B][2][read_length] fp32 (device): the network input (MeasurementRecord.hist); the rest as
+ * qc_actor_act */
+int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs, int32_t noisy,
+                  const float* noise, double eps, uint64_t counter, int32_t* actions, float* q_out,
+                  int32_t* random_out);
+
 /* ---------------------------------------------------------------------------------------------
  * Prioritized experience replay on the device: the reference's SumTree + Memory
  * (inverted harmonic oscillator/RL.py:234-475), fed by BatchedEnv without leaving HBM.

@@ -70,3 +70,33 @@ def forward(params, obs, noise=None, n_actions: int = 21):
 def f_noise(z):
     """layers.py:77-79"""
     return np.sign(z) * np.sqrt(np.abs(z))
+
+
+# ---- DQN_measurement (RL.py:29-78): conv1 -> relu -> conv2 -> relu -> conv3 -> relu -> view -> fc1 -> relu
+#      -> fc21 (noisy) -> relu -> fc31 (noisy)
+M_CONV = ((13, 5), (11, 4), (9, 4))   # (kernel, stride) of conv1..3, no padding
+
+
+def conv1d(x, w, b, stride):
+    """F.conv1d(x [B, ci, L], w [co, ci, k], b, stride) without padding, fp64."""
+    k = w.shape[2]
+    win = np.lib.stride_tricks.sliding_window_view(x, k, axis=2)[:, :, ::stride, :]   # [B, ci, T, k]
+    return np.einsum("bctk,ock->bot", win, w, optimize=True) + b[None, :, None]
+
+
+def forward_measurement(params, obs, noise=None, n_actions: int = 21):
+    """Action values [B, n_actions] for obs [B, 2, L]; noise [B, 789] (f-transformed) or None."""
+    x = np.asarray(obs, dtype=np.float64)
+    for j, (_, s) in enumerate(M_CONV):
+        x = np.maximum(conv1d(x, _np(params[f"conv{j + 1}.weight"]), _np(params[f"conv{j + 1}.bias"]), s), 0.0)
+    x = x.reshape(x.shape[0], -1)
+    x = np.maximum(x @ _np(params["fc1.weight"]).T + _np(params["fc1.bias"]), 0.0)
+    h = 256
+    if noise is not None:
+        nz = np.asarray(noise, dtype=np.float64)
+        e_in21, e_out21 = nz[:, :h], nz[:, h:2 * h]
+        e_in31, e_out31 = nz[:, 2 * h:3 * h], nz[:, 3 * h:3 * h + n_actions]
+    else:
+        e_in21 = e_out21 = e_in31 = e_out31 = None
+    x = np.maximum(_apply(layer(params, "fc21"), x, e_in21, e_out21), 0.0)
+    return _apply(layer(params, "fc31"), x, e_in31, e_out31)

@@ -33,7 +33,7 @@ clean:
 	rm -rf $(CSRC)/build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean resource-usage
+.PHONY: all oracle clean resource-usage expt expt_actor
 
 # experiment builds (not shipped): make expt EXPT=-DQCART_EXPT_NOLOAD NAME=noload
 EXPT ?=
@@ -42,3 +42,8 @@ expt:
 	@mkdir -p $(CSRC)/build_$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(EXPT) -c $(CSRC)/qcart_k_iho.hip -o $(CSRC)/build_$(NAME)/qcart_k_iho.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/qcart_k_iho.o $(filter-out $(CSRC)/build/qcart_k_iho.o,$(OBJS))
+# actor experiment builds: make expt_actor EXPT='-DQCART_MCONV_Q=4' NAME=q4
+expt_actor:
+	@mkdir -p $(CSRC)/build_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(EXPT) -c $(CSRC)/qcart_actor.hip -o $(CSRC)/build_$(NAME)/qcart_actor.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/qcart_actor.o $(filter-out $(CSRC)/build/qcart_actor.o,$(OBJS))

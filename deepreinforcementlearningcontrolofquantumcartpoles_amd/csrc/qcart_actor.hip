@@ -260,8 +260,10 @@ __global__ __launch_bounds__(256) void k_actor_transpose(const float* in, float*
 }
 
 // effective weight (W g / ||W||_F, or W) -> fragments [tile][step][64]; bias padded to tiles*32
+// split = 0: MFMA k-step s pairs k = 2s, 2s + 1 (lane halves); split = 1: k = s, s + Kpad / 2 (the
+// convolutions: the upper half of K is then a fixed input offset, see k_mconv)
 __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float* g, int O, int K, int Kpad,
-                                                     float* frag, const float* bias, float* bias_pad) {
+                                                     float* frag, const float* bias, float* bias_pad, int split) {
     __shared__ double part[1024];
     double ss = 0.0;
     if (g) {
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float
     const int T = tiles(O), S = ksteps(Kpad);
     for (int i = threadIdx.x; i < T * S * 64; i += 1024) {
         const int l = i & 63, s = (i >> 6) % S, t = (i >> 6) / S;
-        const int o = t * 32 + (l & 31), k = 2 * s + (l >> 5);
+        const int o = t * 32 + (l & 31), k = split ? s + (l >> 5) * S : 2 * s + (l >> 5);
         frag[i] = (o < O && k < K) ? W[(size_t)o * K + k] * sc : 0.f;
     }
     if (bias_pad)
@@ -289,82 +291,120 @@ __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float
 // N = (env, position) flattened (32 columns per wave), K = ci * KS in pairs (k = ci * KS + j, the
 // PyTorch weight order). A = weight fragments (k_actor_prep order), B = the input gathered per lane
 // from HBM / L2 (column base X[b] + S t; row offset ci * Tin + j, wave-uniform per k-step half).
-// Loads run a batch of kQ steps ahead of the MFMAs. Output: env-major [b][co][t] (layers 1, 2) or
-// feature-major [co * Tout + t][y_ld] at env column y_off + b (layer 3: fc1's B operand, coalesced).
-constexpr int kQ = 8;
-constexpr int kNT = 2;   // column tiles per wave: every weight fragment feeds kNT MFMAs
-template <int CI, int KS, int S, int MT>
+// Loads run one batch of kQ k-steps ahead of the MFMAs (two register sets, no copies); every load is
+// unconditional (columns past the end read the workgroup's first env, whose results are not stored).
+// Output: env-major [b][co][t] (layers 1, 2) or feature-major [co * Tout + t][y_ld] at env column
+// y_off + b (layer 3: fc1's B operand, coalesced). NT column tiles per wave: every weight fragment feeds
+// NT MFMAs, every input value MT. (A polyphase activation layout that turns the stride-S gathers into
+// contiguous runs was measured: conv2/conv3 unchanged, conv1's scattered stores +23 %; not kept.)
+#ifndef QCART_MCONV_NT
+#define QCART_MCONV_NT 2, 2, 1
+#endif
+constexpr int kNTs[3] = {QCART_MCONV_NT};
+constexpr int kNT1 = kNTs[0], kNT2 = kNTs[1], kNT3 = kNTs[2];
+#ifndef QCART_MCONV_NA
+#define QCART_MCONV_NA 2, 1, 2
+#endif
+constexpr int kNAs[3] = {QCART_MCONV_NA};
+constexpr int kNA1 = kNAs[0], kNA2 = kNAs[1], kNA3 = kNAs[2];
+#ifndef QCART_MCONV_Q
+#define QCART_MCONV_Q 8
+#endif
+constexpr int kQ = QCART_MCONV_Q;
+template <int CI, int KS, int S, int MT, int NT, int NA, bool OUT_FEAT>
 __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int Tin, const float* __restrict__ Wf,
                                                const float* __restrict__ bias, float* __restrict__ Y, int Tout,
-                                               int64_t n_total, int feat_major, int64_t y_ld, int64_t y_off) {
-    constexpr int K = CI * KS, STEPS = (K + 1) / 2;
+                                               int64_t n_total, int64_t y_ld, int64_t y_off) {
+    constexpr int K = CI * KS, STEPS = K / 2;
+    static_assert(CI % 2 == 0, "split-K pairing: k and k + K/2 are channels ci and ci + CI/2");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int hi = lane >> 5;
-    bool col_ok[kNT];
-    int64_t bb[kNT];
-    int tt[kNT];
-    const float* xc[kNT];
+    // buffer descriptor at the workgroup's first env: every lane offset is a small 32-bit VGPR, the
+    // k-step's row offset is wave-uniform (SGPR), so a load costs no VALU
+    const int64_t b0 = (int64_t)blockIdx.x * 128 * NT / Tout;
+    const rsrc_t rx = make_rsrc(X + b0 * CI * Tin, 0xFFFFFFFFu);
+    const rsrc_t rw = make_rsrc(Wf, 0xFFFFFFFFu);
+    bool col_ok[NT];
+    int64_t bb[NT];
+    int tt[NT];
+    int vx[NT];
 #pragma unroll
-    for (int c = 0; c < kNT; ++c) {
-        const int64_t n = (((int64_t)blockIdx.x * 4 + wave) * kNT + c) * 32 + (lane & 31);
+    for (int c = 0; c < NT; ++c) {
+        const int64_t n = (((int64_t)blockIdx.x * 4 + wave) * NT + c) * 32 + (lane & 31);
         col_ok[c] = n < n_total;
-        bb[c] = col_ok[c] ? n / Tout : 0;
+        bb[c] = col_ok[c] ? n / Tout : b0;
         tt[c] = col_ok[c] ? (int)(n - bb[c] * Tout) : 0;
-        xc[c] = X + bb[c] * (int64_t)CI * Tin + (int64_t)S * tt[c];
+        vx[c] = (int)(((bb[c] - b0) * CI * Tin + S * tt[c] + hi * (CI / 2) * Tin) * 4);
     }
-    auto xoff = [&](int s) -> int {   // row offset of k = 2 s + hi: ci * Tin + j
-        const int k = 2 * s + hi;
-        return (k / KS) * Tin + (k % KS);
+    const int vw = lane * 4;
+    // NA accumulator sets for alternating k-steps: NA * MT * NT independent MFMA chains (an MFMA that
+    // accumulates onto the previous one's result waits for it)
+    f32x16 acc[NA][MT][NT];
+#pragma unroll
+    for (int q = 0; q < NA; ++q)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int c = 0; c < NT; ++c) acc[q][m][c] = f32x16{};
+    // k-step s pairs k = s (lanes 0-31) and k = s + K/2 (lanes 32-63); clamped into range (a prefetch
+    // past the end reloads the last step, unused)
+    auto fetch = [&](int s, float (&x)[kQ][NT], float (&w)[kQ][MT]) {
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) {
+            const int sc = min(s + u, STEPS - 1);
+            const int so = ((sc / KS) * Tin + sc % KS) * 4;   // ci * Tin + j
+#pragma unroll
+            for (int c = 0; c < NT; ++c) x[u][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, vx[c], so, 0));
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                w[u][m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, vw, (m * STEPS + sc) * 256, 0));
+        }
     };
-    f32x16 acc[MT][kNT];
+    auto mma = [&](int n, const float (&x)[kQ][NT], const float (&w)[kQ][MT]) {
+#pragma unroll
+        for (int u = 0; u < kQ; ++u)
+            if (u < n)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int c = 0; c < NT; ++c)
+                        acc[u % NA][m][c] =
+                            __builtin_amdgcn_mfma_f32_32x32x2f32(w[u][m], x[u][c], acc[u % NA][m][c], 0, 0, 0);
+    };
+    float xa[kQ][NT], wa[kQ][MT], xb[kQ][NT], wb[kQ][MT];
+    fetch(0, xa, wa);
+    int s = 0;
+    // sched_barriers pin the order: the next batch's loads are issued before this batch's MFMAs
+    for (; s + 2 * kQ <= STEPS; s += 2 * kQ) {
+        fetch(s + kQ, xb, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(kQ, xa, wa);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(s + 2 * kQ, xa, wa);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(kQ, xb, wb);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (s + kQ <= STEPS) {   // one full batch (in xa) and a partial one
+        fetch(s + kQ, xb, wb);
+        mma(kQ, xa, wa);
+        mma(STEPS - s - kQ, xb, wb);
+    } else {
+        mma(STEPS - s, xa, wa);
+    }
+#pragma unroll
+    for (int q = 1; q < NA; ++q)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int c = 0; c < NT; ++c) acc[0][m][c] += acc[q][m][c];
+    float bv[MT][16];   // bias of this lane's output rows, loaded as one batch before the stores
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int c = 0; c < kNT; ++c) acc[m][c] = f32x16{};
-    const float* wl = Wf + lane;
-    constexpr int FULL = STEPS / kQ * kQ;
-    float xb[kQ][kNT], wb[kQ][MT];
-    auto fetch = [&](int s, float (&x)[kNT], float (&w)[MT]) {
-        const bool ok = s < STEPS && 2 * s + hi < K;
-        const int o = ok ? xoff(s) : 0;
+        for (int r = 0; r < 16; ++r) bv[m][r] = bias[m * 32 + drow(r, lane)];
 #pragma unroll
-        for (int c = 0; c < kNT; ++c) x[c] = (ok && col_ok[c]) ? xc[c][o] : 0.f;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) w[m] = s < STEPS ? wl[((int64_t)m * STEPS + s) * 64] : 0.f;
-    };
-#pragma unroll
-    for (int u = 0; u < kQ; ++u) fetch(u, xb[u], wb[u]);
-    for (int s = 0; s < FULL; s += kQ) {
-        float xn[kQ][kNT], wn[kQ][MT];
-#pragma unroll
-        for (int u = 0; u < kQ; ++u) fetch(s + kQ + u, xn[u], wn[u]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < kQ; ++u)
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-                for (int c = 0; c < kNT; ++c)
-                    acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u][c], acc[m][c], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < kQ; ++u) {
-#pragma unroll
-            for (int c = 0; c < kNT; ++c) xb[u][c] = xn[u][c];
-#pragma unroll
-            for (int m = 0; m < MT; ++m) wb[u][m] = wn[u][m];
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < kQ; ++u)
-        if (FULL + u < STEPS)
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-                for (int c = 0; c < kNT; ++c)
-                    acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u][c], acc[m][c], 0, 0, 0);
-#pragma unroll
-    for (int c = 0; c < kNT; ++c) {
+    for (int c = 0; c < NT; ++c) {
         if (!col_ok[c]) continue;
         const int64_t b = bb[c];
         const int t = tt[c];
@@ -373,8 +413,8 @@ __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int co = m * 32 + drow(r, lane);
-                const float v = fmaxf(acc[m][c][r] + bias[co], 0.f);
-                if (feat_major) Y[((int64_t)co * Tout + t) * y_ld + y_off + b] = v;
+                const float v = fmaxf(acc[0][m][c][r] + bv[m][r], 0.f);
+                if constexpr (OUT_FEAT) Y[((int64_t)co * Tout + t) * y_ld + y_off + b] = v;
                 else Y[(b * (MT * 32) + co) * (int64_t)Tout + t] = v;
             }
     }
@@ -571,11 +611,11 @@ int qc_actor_load(qc_actor* a, const qc_dqn_layer layers[4]) {
     for (int l = 0; l < 4; ++l) {
         const qc_dqn_layer& L = layers[l];
         hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.weight, L.weight_norm, O[l], K[l], Kp[l],
-                           w + a->off_u[l], L.bias, w + a->off_ub[l]);
+                           w + a->off_u[l], L.bias, w + a->off_ub[l], 0);
         a->has_s[l] = L.sigma_w != nullptr;
         if (L.sigma_w)
             hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.sigma_w, (const float*)nullptr, O[l],
-                               K[l], Kp[l], w + a->off_s[l], L.sigma_b, w + a->off_sb[l]);
+                               K[l], Kp[l], w + a->off_s[l], L.sigma_b, w + a->off_sb[l], 0);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(a, e, "actor weight preparation");
@@ -678,7 +718,7 @@ int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out) {
     }
     a->flat = kC3 * a->T3;
     a->noise_len = 2 * kH2 + kH3 + p->n_actions;
-    a->chunk = (int)std::min<int64_t>(p->max_batch, p->chunk > 0 ? p->chunk : 1024);
+    a->chunk = (int)std::min<int64_t>(p->max_batch, p->chunk > 0 ? p->chunk : 2048);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete a;
@@ -767,10 +807,10 @@ int qc_mactor_load(qc_mactor* a, const qc_dqn_layer layers[6]) {
         const qc_dqn_layer& L = layers[l];
         const int Kp = (K[l] + 1) & ~1;
         hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.weight, L.weight_norm, O[l], K[l], Kp,
-                           w + a->off_w[l], L.bias, w + a->off_b[l]);
+                           w + a->off_w[l], L.bias, w + a->off_b[l], l < 3 ? 1 : 0);
         if (l >= 4 && L.sigma_w)
             hipLaunchKernelGGL(k_actor_prep, dim3(1), dim3(1024), 0, a->stream, L.sigma_w, (const float*)nullptr, O[l],
-                               K[l], Kp, w + a->off_s[l], L.sigma_b, w + a->off_sb[l]);
+                               K[l], Kp, w + a->off_s[l], L.sigma_b, w + a->off_sb[l], 0);
     }
     a->has_s21 = layers[4].sigma_w != nullptr;
     a->has_s31 = layers[5].sigma_w != nullptr;
@@ -797,14 +837,15 @@ int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs,
     for (int64_t c0 = 0; c0 < B; c0 += a->chunk) {   // conv stack per env chunk (its activations stay in L2 / MALL)
         const int64_t nb = std::min<int64_t>(a->chunk, B - c0);
         const int64_t n1 = nb * a->T1, n2 = nb * a->T2, n3 = nb * a->T3;
-        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1>), dim3((unsigned)((n1 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
-                           obs + c0 * 2 * L, L, w + a->off_w[0], w + a->off_b[0], a->d_y1, a->T1, n1, 0, (int64_t)0,
-                           (int64_t)0);
-        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2>), dim3((unsigned)((n2 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
-                           a->d_y1, a->T1, w + a->off_w[1], w + a->off_b[1], a->d_y2, a->T2, n2, 0, (int64_t)0,
-                           (int64_t)0);
-        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2>), dim3((unsigned)((n3 + 128 * kNT - 1) / (128 * kNT))), dim3(256), 0, a->stream,
-                           a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3, a->T3, n3, 1, ld, c0);
+        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1, kNT1, kNA1, false>), dim3((unsigned)((n1 + 128 * kNT1 - 1) / (128 * kNT1))),
+                           dim3(256), 0, a->stream, obs + c0 * 2 * L, L, w + a->off_w[0], w + a->off_b[0], a->d_y1,
+                           a->T1, n1, (int64_t)0, (int64_t)0);
+        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2, kNT2, kNA2, false>), dim3((unsigned)((n2 + 128 * kNT2 - 1) / (128 * kNT2))),
+                           dim3(256), 0, a->stream, a->d_y1, a->T1, w + a->off_w[1], w + a->off_b[1], a->d_y2, a->T2,
+                           n2, (int64_t)0, (int64_t)0);
+        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2, kNT3, kNA3, true>), dim3((unsigned)((n3 + 128 * kNT3 - 1) / (128 * kNT3))),
+                           dim3(256), 0, a->stream, a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3, a->T3,
+                           n3, ld, c0);
     }
     hipLaunchKernelGGL(k_mfc, dim3((unsigned)((B + 127) / 128)), dim3(256), 0, a->stream, a->d_y3, ld, a->flat,
                        w + a->off_w[3], w + a->off_b[3], a->d_h1, B);

@@ -276,7 +276,7 @@ typedef struct qc_mdqn_params {
     int32_t n_actions;     /* 21 */
     int64_t max_batch;
     uint64_t seed;
-    int32_t chunk;         /* envs per convolution chunk (0: 1024) */
+    int32_t chunk;         /* envs per convolution chunk (0: 2048) */
 } qc_mdqn_params;
 typedef struct qc_mactor qc_mactor;
 int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out);

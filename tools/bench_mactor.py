@@ -50,11 +50,11 @@ def main():
     fl = flops_per_env(L) * B
     print(json.dumps({"metric": "measurement-input DQN actor decisions/s (one qc_mactor_act over the batch)",
                       "value": B / ms * 1e3, "unit": "decisions/s", "batch": B, "ms_per_call": ms, "dtype": "f32",
-                      "chunk": args.chunk or 1024,
+                      "chunk": args.chunk or 2048,
                       "roofline": {"bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12,
                                    "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
                                    "frac": fl / (ms * 1e-3) / PEAK_F32_MFMA, "flops_per_decision": flops_per_env(L)},
-                      "note": "conv1..3 implicit GEMMs per env chunk + fc1 GEMM + noisy tail, in-kernel noise"}),
+                      "note": "conv1..3 implicit GEMMs (buffer loads, split-K pairing) per env chunk + fc1 GEMM + noisy tail, in-kernel noise"}),
           flush=True)
 
 

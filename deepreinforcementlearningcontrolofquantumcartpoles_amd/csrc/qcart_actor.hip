@@ -293,9 +293,10 @@ __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float
 // from HBM / L2 (column base X[b] + S t; row offset ci * Tin + j, wave-uniform per k-step half).
 // Loads run one batch of kQ k-steps ahead of the MFMAs (two register sets, no copies); every load is
 // unconditional (columns past the end read the workgroup's first env, whose results are not stored).
-// Output: env-major [b][co][t] (layers 1, 2) or feature-major [co * Tout + t][y_ld] at env column
-// y_off + b (layer 3: fc1's B operand, coalesced). NT column tiles per wave: every weight fragment feeds
-// NT MFMAs, every input value MT. (A polyphase activation layout that turns the stride-S gathers into
+// Output: env-major [b][co][t] (32 consecutive t per store: one 128-B run); conv3's is transposed
+// afterwards by k_mtr into fc1's feature-major operand (written directly, every lane's store hit its own
+// cache line: 4.6 M partial-line writes per chunk). NT column tiles per wave: every weight fragment
+// feeds NT MFMAs, every input value MT. (A polyphase activation layout that turns the stride-S gathers into
 // contiguous runs was measured: conv2/conv3 unchanged, conv1's scattered stores +23 %; not kept.)
 #ifndef QCART_MCONV_NT
 #define QCART_MCONV_NT 2, 2, 1
@@ -311,10 +312,10 @@ constexpr int kNA1 = kNAs[0], kNA2 = kNAs[1], kNA3 = kNAs[2];
 #define QCART_MCONV_Q 8
 #endif
 constexpr int kQ = QCART_MCONV_Q;
-template <int CI, int KS, int S, int MT, int NT, int NA, bool OUT_FEAT>
+template <int CI, int KS, int S, int MT, int NT, int NA>
 __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int Tin, const float* __restrict__ Wf,
                                                const float* __restrict__ bias, float* __restrict__ Y, int Tout,
-                                               int64_t n_total, int64_t y_ld, int64_t y_off) {
+                                               int64_t n_total) {
     constexpr int K = CI * KS, STEPS = K / 2;
     static_assert(CI % 2 == 0, "split-K pairing: k and k + K/2 are channels ci and ci + CI/2");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -414,9 +415,26 @@ __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int 
             for (int r = 0; r < 16; ++r) {
                 const int co = m * 32 + drow(r, lane);
                 const float v = fmaxf(acc[0][m][c][r] + bv[m][r], 0.f);
-                if constexpr (OUT_FEAT) Y[((int64_t)co * Tout + t) * y_ld + y_off + b] = v;
-                else Y[(b * (MT * 32) + co) * (int64_t)Tout + t] = v;
+                Y[(b * (MT * 32) + co) * (int64_t)Tout + t] = v;
             }
+    }
+}
+
+// conv3's env-major chunk output [nb][F] -> fc1's feature-major operand [F][ld] at env column c0: 64x64
+// tiles through LDS, coalesced on both sides
+__global__ __launch_bounds__(256) void k_mtr(const float* __restrict__ in, float* __restrict__ out, int F,
+                                             int64_t nb, int64_t ld, int64_t c0) {
+    __shared__ float t[64][65];
+    const int64_t b0 = (int64_t)blockIdx.y * 64;
+    const int f0 = blockIdx.x * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t b = b0 + r;
+        t[r][tx] = (b < nb && f0 + tx < F) ? in[b * F + f0 + tx] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int f = f0 + r;
+        if (f < F && b0 + tx < nb) out[(int64_t)f * ld + c0 + b0 + tx] = t[tx][r];
     }
 }
 
@@ -684,7 +702,7 @@ struct qc_mactor {
     bool loaded = false, has_s21 = false, has_s31 = false;
     float* d_w = nullptr;
     size_t off_w[6]{}, off_b[6]{}, off_s[6]{}, off_sb[6]{};
-    float *d_y1 = nullptr, *d_y2 = nullptr, *d_y3 = nullptr, *d_h1 = nullptr, *d_noise = nullptr;
+    float *d_y1 = nullptr, *d_y2 = nullptr, *d_y3e = nullptr, *d_y3 = nullptr, *d_h1 = nullptr, *d_noise = nullptr;
 };
 
 namespace {
@@ -746,6 +764,7 @@ int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out) {
     if (e == hipSuccess) e = hipMemset(a->d_w, 0, off * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&a->d_y1, ch * kC1 * a->T1 * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&a->d_y2, ch * kC2 * a->T2 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&a->d_y3e, (size_t)a->flat * ch * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&a->d_y3, (size_t)a->flat * mb * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&a->d_h1, (size_t)kH2 * mb * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&a->d_noise, (size_t)a->noise_len * mb * sizeof(float));
@@ -766,7 +785,7 @@ void qc_mactor_destroy(qc_mactor* a) {
     {
         Dev g(a->device);
         (void)hipDeviceSynchronize();
-        for (float* q : {a->d_w, a->d_y1, a->d_y2, a->d_y3, a->d_h1, a->d_noise})
+        for (float* q : {a->d_w, a->d_y1, a->d_y2, a->d_y3e, a->d_y3, a->d_h1, a->d_noise})
             if (q) (void)hipFree(q);
     }
     delete a;
@@ -837,15 +856,17 @@ int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs,
     for (int64_t c0 = 0; c0 < B; c0 += a->chunk) {   // conv stack per env chunk (its activations stay in L2 / MALL)
         const int64_t nb = std::min<int64_t>(a->chunk, B - c0);
         const int64_t n1 = nb * a->T1, n2 = nb * a->T2, n3 = nb * a->T3;
-        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1, kNT1, kNA1, false>), dim3((unsigned)((n1 + 128 * kNT1 - 1) / (128 * kNT1))),
+        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1, kNT1, kNA1>), dim3((unsigned)((n1 + 128 * kNT1 - 1) / (128 * kNT1))),
                            dim3(256), 0, a->stream, obs + c0 * 2 * L, L, w + a->off_w[0], w + a->off_b[0], a->d_y1,
-                           a->T1, n1, (int64_t)0, (int64_t)0);
-        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2, kNT2, kNA2, false>), dim3((unsigned)((n2 + 128 * kNT2 - 1) / (128 * kNT2))),
+                           a->T1, n1);
+        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2, kNT2, kNA2>), dim3((unsigned)((n2 + 128 * kNT2 - 1) / (128 * kNT2))),
                            dim3(256), 0, a->stream, a->d_y1, a->T1, w + a->off_w[1], w + a->off_b[1], a->d_y2, a->T2,
-                           n2, (int64_t)0, (int64_t)0);
-        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2, kNT3, kNA3, true>), dim3((unsigned)((n3 + 128 * kNT3 - 1) / (128 * kNT3))),
-                           dim3(256), 0, a->stream, a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3, a->T3,
-                           n3, ld, c0);
+                           n2);
+        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2, kNT3, kNA3>), dim3((unsigned)((n3 + 128 * kNT3 - 1) / (128 * kNT3))),
+                           dim3(256), 0, a->stream, a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3e, a->T3,
+                           n3);
+        hipLaunchKernelGGL(k_mtr, dim3((unsigned)((a->flat + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,
+                           a->stream, a->d_y3e, a->d_y3, a->flat, nb, ld, c0);
     }
     hipLaunchKernelGGL(k_mfc, dim3((unsigned)((B + 127) / 128)), dim3(256), 0, a->stream, a->d_y3, ld, a->flat,
                        w + a->off_w[3], w + a->off_b[3], a->d_h1, B);

@@ -195,7 +195,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if fp32 else "f64",
-        "data": "synthetic (random psi0 on Fock levels < 16; actions ~ U{0..20} per control step)",
+        "data": ("synthetic (random psi0 on Fock levels < 16; actions ~ U{0..20} per control step)" if ph.fock else
+                 "synthetic (Gaussian packets mu~U[-1,1], sigma~U[0.7,1.3], k~U[-0.3,0.3]; actions ~ U{0..20} "
+                 "per control step)"),
         "config": {"workload": f"{cfg.FAMILY_NAMES[ph.family]} N={N} per-GPU batch={B} "
                                f"{n_sub} physics steps + moments per step ({args.config})",
                    "global_batch": B * world, "seq_len": N, "parallelism": f"env-shard{world}",

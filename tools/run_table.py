@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""BASELINE.md §4 run table from the per-config bench lines (profiles/r01_<cfg>_bench_line.json) and
+rocprofv3 summaries (profiles/r01_<cfg>_summary.json) written by tools/run_table.sh + prof_summary.py.
+Prints a markdown table and writes profiles/r01_run_table.json."""
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROWS = [("C1 HO cooling", "C1"), ("C2 IHO cartpole", "C2"), ("C3 QO cooling", "C3"),
+        ("C4 IQO cartpole (per GPU of 8)", "C4"), ("C5 IHO stress (per GPU of 8)", "C5"), ("Metric IHO", "metric")]
+
+
+def main(tag="r01"):
+    prof = os.path.join(ROOT, "profiles")
+    out = []
+    print("| config | N | B per GPU | dtype | env-steps/s (1 GPU) | k_step ms/launch | HBM-roofline frac "
+          "(algorithmic) | FP-VALU frac | rocprof HBM GB/s | CPU baseline env-steps/s (threads) |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
+    for name, c in ROWS:
+        bl = json.loads(open(os.path.join(prof, f"{tag}_{c}_bench_line.json")).read())
+        sm = json.load(open(os.path.join(prof, f"{tag}_{c}_summary.json")))
+        rf, cpu = bl["roofline"], bl.get("cpu_baseline", {})
+        hbm = sm.get("hbm_bytes_per_launch")
+        gbs = hbm / (sm["avg_ms"] * 1e-3) / 1e9 if hbm else None
+        row = {"config": c, "N": bl["config"]["seq_len"], "batch": bl["config"]["global_batch"], "dtype": bl["dtype"],
+               "env_steps_per_s": bl["value"], "kernel_ms": rf["kernel_ms"], "prof_kernel_ms": sm["avg_ms"],
+               "hbm_frac": rf["frac"], "valu_frac": bl["valu"]["frac"], "rocprof_hbm_gbs": gbs,
+               "cpu_env_steps_per_s": cpu.get("value"), "cpu_threads": cpu.get("cores"),
+               "cpu_single_core": cpu.get("single_core_value")}
+        out.append(row)
+        print(f"| {name} | {row['N']} | {row['batch']} | {row['dtype']} | {row['env_steps_per_s']:.3g} | "
+              f"{row['kernel_ms']:.3g} | {row['hbm_frac']:.3f} | {row['valu_frac']:.3f} | "
+              f"{gbs:.0f} | {row['cpu_env_steps_per_s']:.3g} ({row['cpu_threads']}) |")
+    json.dump(out, open(os.path.join(prof, f"{tag}_run_table.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

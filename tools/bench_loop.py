@@ -4,8 +4,11 @@ DQNActor (direct_DQN, random-initialised weights of the reference architecture) 
 act -> step (80 physics steps) -> experience rows stored in the device prioritized replay (the drivers'
 capacity 7000 x 18 x 100 = 12.6 M rows, qc_replay_store_xp) -> one sample(512) + batch_update, the
 trainer's per-step memory traffic (RL.py:172, :224), with auto-reset of finished episodes.
+With --input measurements: BatchedEnv(input='measurements') (the measurement record, qc_record) +
+MeasurementActor (DQN_measurement) + the replay storing the reference's 5 915-float rows (capacity
+--capacity rows; the drivers' 2.7 M-row memory is 64 GB, the bench default keeps 262 144 rows).
 Prints one JSON line: RL steps/s (decisions), env-steps/s and the actor's / replay's share of the loop.
-usage: python tools/bench_loop.py [--batch B] [--steps K]"""
+usage: python tools/bench_loop.py [--batch B] [--steps K] [--input xp|measurements]"""
 import argparse
 import json
 import os
@@ -17,7 +20,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
-from deepreinforcementlearningcontrolofquantumcartpoles_amd.actor import DQNActor, random_direct_dqn  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.actor import (  # noqa: E402
+    DQNActor, MeasurementActor, random_direct_dqn, random_dqn_measurement)
 from deepreinforcementlearningcontrolofquantumcartpoles_amd.env import BatchedEnv  # noqa: E402
 from deepreinforcementlearningcontrolofquantumcartpoles_amd.replay import PrioritizedReplay  # noqa: E402
 
@@ -27,13 +31,20 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--capacity", type=int, default=7000 * 18 * 100)   # IHO/arguments.py:80, main_parallel.py:595
+    ap.add_argument("--capacity", type=int, default=0)   # xp: 7000 x 18 x 100 (IHO/arguments.py:80, main_parallel.py:595)
+    ap.add_argument("--input", choices=("xp", "measurements"), default="xp")
     args = ap.parse_args()
     B = args.batch
+    meas = args.input == "measurements"
     ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)
-    env = BatchedEnv(ph, B, 0, seed=1)
-    actor = DQNActor({k: v.cuda() for k, v in random_direct_dqn(seed=1).items()}, max_batch=B, seed=2)
-    mem = PrioritizedReplay(args.capacity, 2 * 5 + 2, "random", 0.2, device=0, seed=3)
+    env = BatchedEnv(ph, B, 0, seed=1, input=args.input)
+    if meas:
+        actor = MeasurementActor({k: v.cuda() for k, v in random_dqn_measurement(seed=1).items()}, max_batch=B, seed=2)
+        row_len = int(env.rows.shape[1])
+        mem = PrioritizedReplay(args.capacity or 262144, row_len, "random", 0.2, device=0, seed=3)
+    else:
+        actor = DQNActor({k: v.cuda() for k, v in random_direct_dqn(seed=1).items()}, max_batch=B, seed=2)
+        mem = PrioritizedReplay(args.capacity or 7000 * 18 * 100, 2 * 5 + 2, "random", 0.2, device=0, seed=3)
     obs = env.reset()
     steps_done = 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,7 +64,10 @@ def main():
         obs, reward, done, info = env.step(a)
         rows += int(info["valid"].sum())
         r0.record()
-        mem.store_xp(info["last_obs"], obs, a, reward, info["valid"])
+        if meas:
+            mem.store(info["rows"], info["valid"])
+        else:
+            mem.store_xp(info["last_obs"], obs, a, reward, info["valid"])
         smp = mem.obtain_sample(512) if it > 0 else None
         if smp is not None:
             mem.batch_update(smp[0], torch.rand(512, device="cuda"))
@@ -64,14 +78,16 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     K = args.steps
-    print(json.dumps({"metric": "actor loop RL steps/s (BatchedEnv IHO N=512 + device DQN actor)",
+    net = "DQN_measurement" if meas else "direct_DQN"
+    print(json.dumps({"metric": f"actor loop RL steps/s (BatchedEnv IHO N=512 input={args.input} + device {net} actor)",
                       "value": B * K / dt, "unit": "decisions/s", "env_steps_per_s": B * K * ph.control_interval / dt,
                       "batch": B, "control_steps": K, "ms_per_control_step": dt / K * 1e3,
                       "actor_ms_per_control_step": actor_ms / K, "actor_share": actor_ms / (dt * 1e3),
                       "replay_ms_per_control_step": replay_ms / K, "replay_share": replay_ms / (dt * 1e3),
                       "replay_len": len(mem),
                       "experience_rows_per_s": rows / dt,
-                      "data": "synthetic: |0> resets, random-initialised direct_DQN weights"}), flush=True)
+                      "row_len": mem.data_size,
+                      "data": f"synthetic: |0> resets, random-initialised {net} weights"}), flush=True)
 
 
 if __name__ == "__main__":

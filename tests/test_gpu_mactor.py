@@ -84,3 +84,28 @@ def test_mactor_drives_the_measurement_env():
         assert a.dtype == torch.int32 and bool(((a >= 0) & (a < 21)).all())
         obs, r, done, info = env.step(a)
     assert obs.shape == (64, 2, 5760)
+
+
+def test_mactor_edge_cases_and_reload():
+    """B = 0 is a no-op; wrong shapes and B > max_batch are refused; a weight of the wrong shape is refused
+    at load; reloading other weights changes the answer to the oracle's for those weights."""
+    L, B = 4320, 16
+    p = random_dqn_measurement(read_length=L, seed=30)
+    actor = MeasurementActor({k: v.cuda() for k, v in p.items()}, read_length=L, max_batch=B, seed=1)
+    a0 = actor.act(torch.zeros((0, 2, L), device="cuda"))
+    assert a0.shape == (0,)
+    with pytest.raises(ValueError):
+        actor.act(torch.zeros((B + 1, 2, L), device="cuda"))
+    with pytest.raises(ValueError):
+        actor.act(torch.zeros((4, 2, L - 1), device="cuda"))
+    with pytest.raises(ValueError):
+        actor.act(torch.zeros((4, 1, L), device="cuda"))
+    bad = dict(p)
+    bad["fc1.weight"] = torch.zeros(256, 17)
+    with pytest.raises(ValueError):
+        actor.load({k: v.cuda() for k, v in bad.items()})
+    obs = make_records(B, L, seed=5)
+    p2 = random_dqn_measurement(read_length=L, seed=31)
+    actor.load({k: v.cuda() for k, v in p2.items()})
+    act, ex = actor.act(torch.from_numpy(obs).cuda(), noisy=False, want_q=True)
+    check(ex["q"].cpu().numpy(), dqn.forward_measurement(p2, obs.astype(np.float64), None), act.cpu().numpy())

@@ -438,52 +438,117 @@ __global__ __launch_bounds__(256) void k_mtr(const float* __restrict__ in, float
     }
 }
 
-// fc1 (nn.Linear K -> 256) + ReLU for 32 envs per wave: B = the feature-major conv output
-// X[k][x_ld] (one coalesced 128-B row per k-step half), 8 row tiles share each B load.
+// fc1 (nn.Linear K -> 256) + ReLU: B = the feature-major conv output X[k][x_ld] (one coalesced 128-B row
+// per k-step half and column tile). A wave computes MT of the 8 output tiles for NT * 32 envs; the 8 / MT
+// waves that share an env group sit in one workgroup (their B reads coincide in L1 / L2). Weight
+// traffic per env is 8 / (MT * NT) tile streams of K: (MT, NT) = (8, 1) streams the 4.6 MB weight
+// matrix once per 32 envs — more than one XCD's L2, so from MALL. Buffer loads with wave-uniform
+// k-step offsets, batches of kQF k-steps loaded one batch ahead of the MFMAs.
+#ifndef QCART_MFC_MT
+#define QCART_MFC_MT 2
+#endif
+#ifndef QCART_MFC_NT
+#define QCART_MFC_NT 2
+#endif
+constexpr int kMfcMT = QCART_MFC_MT, kMfcNT = QCART_MFC_NT, kQF = 4;
+template <int MT, int NT>
 __global__ __launch_bounds__(256) void k_mfc(const float* __restrict__ X, int64_t x_ld, int K,
                                              const float* __restrict__ Wf, const float* __restrict__ bias,
                                              float* __restrict__ H, int64_t B) {
-    constexpr int MT = 8;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t e = ((int64_t)blockIdx.x * 4 + wave) * 32 + (lane & 31);
-    const bool ok = e < B;
-    const int steps = (K + 1) / 2, hi = lane >> 5;
-    const float* xc = X + (ok ? e : 0);
-    f32x16 acc[MT];
+    constexpr int MP = 8 / MT;   // waves per env group
+    static_assert(4 % MP == 0, "the waves of an env group share a workgroup");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: descriptors stay in SGPRs
+    const int mp = wave % MP;
+    const int64_t e0 = ((int64_t)blockIdx.x * (4 / MP) + wave / MP) * NT * 32;
+    const int steps = K / 2, hi = lane >> 5;   // K = 64 T3 is even
+    const rsrc_t rx = make_rsrc(X + e0, 0xFFFFFFFFu);
+    const rsrc_t rw = make_rsrc(Wf + (size_t)mp * MT * steps * 64, 0xFFFFFFFFu);
+    bool ok[NT];
+    int vx[NT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = f32x16{};
-    const float* wl = Wf + lane;
-    constexpr int Q = 4;
-    int s = 0;
-    for (; s + Q <= steps; s += Q) {
-        float xb[Q], wb[Q][MT];
-#pragma unroll
-        for (int u = 0; u < Q; ++u) {
-            const int k = 2 * (s + u) + hi;
-            xb[u] = (ok && k < K) ? xc[(int64_t)k * x_ld] : 0.f;
-#pragma unroll
-            for (int m = 0; m < MT; ++m) wb[u][m] = wl[((int64_t)m * steps + s + u) * 64];
-        }
-#pragma unroll
-        for (int u = 0; u < Q; ++u)
-#pragma unroll
-            for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[u][m], xb[u], acc[m], 0, 0, 0);
+    for (int c = 0; c < NT; ++c) {
+        const int64_t e = e0 + c * 32 + (lane & 31);
+        ok[c] = e < B;
+        vx[c] = (int)(((ok[c] ? c * 32 + (lane & 31) : 0) + (int64_t)hi * x_ld) * 4);   // row k = 2 s + hi
     }
-    for (; s < steps; ++s) {
-        const int k = 2 * s + hi;
-        const float xv = (ok && k < K) ? xc[(int64_t)k * x_ld] : 0.f;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[((int64_t)m * steps + s) * 64], xv, acc[m], 0, 0, 0);
-    }
-    if (!ok) return;
+    const int vw = lane * 4;
+    f32x16 acc[MT][NT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int o = m * 32 + drow(r, lane);
-            H[(int64_t)o * x_ld + e] = fmaxf(acc[m][r] + bias[o], 0.f);   // feature-major [256][ld]
+        for (int c = 0; c < NT; ++c) acc[m][c] = f32x16{};
+    auto fetch = [&](int s, float (&x)[kQF][NT], float (&w)[kQF][MT]) {
+#pragma unroll
+        for (int u = 0; u < kQF; ++u) {
+            const int sc = min(s + u, steps - 1);
+            const int xo = (int)((uint32_t)(2 * sc) * (uint32_t)x_ld * 4u);   // < 4 GiB: checked at create
+#pragma unroll
+            for (int c = 0; c < NT; ++c) x[u][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, vx[c], xo, 0));
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                w[u][m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, vw, (m * steps + sc) * 256, 0));
         }
+    };
+    auto mma = [&](const float (&x)[kQF][NT], const float (&w)[kQF][MT]) {
+#pragma unroll
+        for (int u = 0; u < kQF; ++u)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int c = 0; c < NT; ++c)
+                    acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[u][m], x[u][c], acc[m][c], 0, 0, 0);
+    };
+    float xa[kQF][NT], wa[kQF][MT], xb[kQF][NT], wb[kQF][MT];
+    // runtime K (= 64 T3 >= 64, so at least one double batch): whole double batches, then single steps
+    const int full = steps / (2 * kQF) * (2 * kQF);
+    int s = 0;
+    fetch(0, xa, wa);
+    do {
+        fetch(s + kQF, xb, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(xa, wa);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(s + 2 * kQF, xa, wa);   // past the end: clamped re-reads, unused
+        __builtin_amdgcn_sched_barrier(0);
+        mma(xb, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        s += 2 * kQF;
+    } while (s < full);
+    for (; s < steps; ++s) {
+        float x1[NT], w1[MT];
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+            x1[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, vx[c], (int)((uint32_t)(2 * s) * (uint32_t)x_ld * 4u), 0));
+#pragma unroll
+        for (int m = 0; m < MT; ++m) w1[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, vw, (m * steps + s) * 256, 0));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int c = 0; c < NT; ++c) acc[m][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[m], x1[c], acc[m][c], 0, 0, 0);
+    }
+    float bv[MT][16];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[m][r] = bias[(mp * MT + m) * 32 + drow(r, lane)];
+    // feature-major [256][ld] through a descriptor at (row 0, env e0): per-lane offset (column, the
+    // lane half's 4-row shift) in a VGPR, the row's offset ((mp MT + m) 32 + (r & 3) + 8 (r >> 2)) x_ld
+    // wave-uniform (SGPR)
+    const rsrc_t rh = make_rsrc(H + e0, 0xFFFFFFFFu);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+        if (!ok[c]) continue;
+        const int vh = (int)((c * 32 + (lane & 31) + (int64_t)4 * hi * x_ld) * 4);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t row = (uint32_t)((mp * MT + m) * 32 + (r & 3) + 8 * (r >> 2));
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaxf(acc[m][c][r] + bv[m][r], 0.f)), rh, vh,
+                                                      (int)(row * (uint32_t)x_ld * 4u), 0);
+            }
+    }
 }
 
 }  // namespace actor
@@ -735,6 +800,10 @@ int qc_mactor_create(const qc_mdqn_params* p, int device, qc_mactor** out) {
         return fail("read_length too short for the three convolutions", QC_EINVAL);
     }
     a->flat = kC3 * a->T3;
+    if ((uint64_t)a->flat * (uint64_t)p->max_batch * sizeof(float) >= (1ull << 32)) {   // 32-bit buffer offsets
+        delete a;
+        return fail("max_batch too large: fc1's operand [64 T3][max_batch] must stay below 4 GiB", QC_EINVAL);
+    }
     a->noise_len = 2 * kH2 + kH3 + p->n_actions;
     a->chunk = (int)std::min<int64_t>(p->max_batch, p->chunk > 0 ? p->chunk : 2048);
     int ndev = 0;
@@ -868,8 +937,11 @@ int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs,
         hipLaunchKernelGGL(k_mtr, dim3((unsigned)((a->flat + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,
                            a->stream, a->d_y3e, a->d_y3, a->flat, nb, ld, c0);
     }
-    hipLaunchKernelGGL(k_mfc, dim3((unsigned)((B + 127) / 128)), dim3(256), 0, a->stream, a->d_y3, ld, a->flat,
-                       w + a->off_w[3], w + a->off_b[3], a->d_h1, B);
+    {
+        constexpr int envs_per_wg = (4 / (8 / kMfcMT)) * kMfcNT * 32;
+        hipLaunchKernelGGL((k_mfc<kMfcMT, kMfcNT>), dim3((unsigned)((B + envs_per_wg - 1) / envs_per_wg)), dim3(256), 0,
+                           a->stream, a->d_y3, ld, a->flat, w + a->off_w[3], w + a->off_b[3], a->d_h1, B);
+    }
     const bool need_noise = noisy && (a->has_s21 || a->has_s31);
     if (need_noise) {
         if (noise) {

@@ -309,10 +309,11 @@ constexpr int kNT1 = kNTs[0], kNT2 = kNTs[1], kNT3 = kNTs[2];
 constexpr int kNAs[3] = {QCART_MCONV_NA};
 constexpr int kNA1 = kNAs[0], kNA2 = kNAs[1], kNA3 = kNAs[2];
 #ifndef QCART_MCONV_Q
-#define QCART_MCONV_Q 8
+#define QCART_MCONV_Q 4, 4, 4
 #endif
-constexpr int kQ = QCART_MCONV_Q;
-template <int CI, int KS, int S, int MT, int NT, int NA>
+constexpr int kQs[3] = {QCART_MCONV_Q};   // k-steps per load batch
+constexpr int kQ1 = kQs[0], kQ2 = kQs[1], kQ3 = kQs[2];
+template <int CI, int KS, int S, int MT, int NT, int NA, int kQ>
 __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int Tin, const float* __restrict__ Wf,
                                                const float* __restrict__ bias, float* __restrict__ Y, int Tout,
                                                int64_t n_total) {
@@ -404,18 +405,20 @@ __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int 
     for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) bv[m][r] = bias[m * 32 + drow(r, lane)];
+    // stores through a descriptor at the workgroup's first env: per-lane offset (env, position, the lane
+    // half's 4-row shift) in a VGPR, the output row's (m 32 + (r & 3) + 8 (r >> 2)) Tout wave-uniform
+    const rsrc_t ry = make_rsrc(Y + b0 * (MT * 32) * Tout, 0xFFFFFFFFu);
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
         if (!col_ok[c]) continue;
-        const int64_t b = bb[c];
-        const int t = tt[c];
+        const int vy = (int)((((bb[c] - b0) * (MT * 32) + 4 * hi) * Tout + tt[c]) * 4);
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int co = m * 32 + drow(r, lane);
-                const float v = fmaxf(acc[0][m][c][r] + bv[m][r], 0.f);
-                Y[(b * (MT * 32) + co) * (int64_t)Tout + t] = v;
+                const int row = m * 32 + (r & 3) + 8 * (r >> 2);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaxf(acc[0][m][c][r] + bv[m][r], 0.f)), ry, vy,
+                                                      row * Tout * 4, 0);
             }
     }
 }
@@ -925,13 +928,13 @@ int qc_mactor_act(qc_mactor* a, int64_t B, int64_t env_offset, const float* obs,
     for (int64_t c0 = 0; c0 < B; c0 += a->chunk) {   // conv stack per env chunk (its activations stay in L2 / MALL)
         const int64_t nb = std::min<int64_t>(a->chunk, B - c0);
         const int64_t n1 = nb * a->T1, n2 = nb * a->T2, n3 = nb * a->T3;
-        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1, kNT1, kNA1>), dim3((unsigned)((n1 + 128 * kNT1 - 1) / (128 * kNT1))),
+        hipLaunchKernelGGL((k_mconv<2, 13, 5, 1, kNT1, kNA1, kQ1>), dim3((unsigned)((n1 + 128 * kNT1 - 1) / (128 * kNT1))),
                            dim3(256), 0, a->stream, obs + c0 * 2 * L, L, w + a->off_w[0], w + a->off_b[0], a->d_y1,
                            a->T1, n1);
-        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2, kNT2, kNA2>), dim3((unsigned)((n2 + 128 * kNT2 - 1) / (128 * kNT2))),
+        hipLaunchKernelGGL((k_mconv<32, 11, 4, 2, kNT2, kNA2, kQ2>), dim3((unsigned)((n2 + 128 * kNT2 - 1) / (128 * kNT2))),
                            dim3(256), 0, a->stream, a->d_y1, a->T1, w + a->off_w[1], w + a->off_b[1], a->d_y2, a->T2,
                            n2);
-        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2, kNT3, kNA3>), dim3((unsigned)((n3 + 128 * kNT3 - 1) / (128 * kNT3))),
+        hipLaunchKernelGGL((k_mconv<64, 9, 4, 2, kNT3, kNA3, kQ3>), dim3((unsigned)((n3 + 128 * kNT3 - 1) / (128 * kNT3))),
                            dim3(256), 0, a->stream, a->d_y2, a->T2, w + a->off_w[2], w + a->off_b[2], a->d_y3e, a->T3,
                            n3);
         hipLaunchKernelGGL(k_mtr, dim3((unsigned)((a->flat + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,

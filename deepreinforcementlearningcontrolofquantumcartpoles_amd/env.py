@@ -73,7 +73,28 @@ class BatchedEnv:
         self.obs = (self.rec.hist if self.rec is not None else
                     torch.zeros((self.B, self.st.n_obs), dtype=torch.float32, device=self.dev))
         self.episode_return = z(torch.float64)
-        self.finished_returns: list = []          # (return, length) of finished episodes (host)
+        # finished episodes (return, length) compacted on the device into a ring of _fin_cap entries
+        # (slot _fin_cap is the sink of the not-finished envs): no boolean indexing, no dynamic shapes and
+        # no host copy per step; read through finished_returns
+        self._fin_cap = max(1 << 16, 16 * self.B)
+        self._fin = torch.zeros((2, self._fin_cap + 1), dtype=torch.float64, device=self.dev)
+        self._fin_n = torch.zeros((), dtype=torch.int64, device=self.dev)
+        self._fin_read = 0
+        self._fin_host: list = []
+
+    @property
+    def finished_returns(self) -> list:
+        """(returns, lengths) float64 CPU tensors of the episodes finished so far, one entry per read
+        that found new ones (the reference's per-actor result queue, main_parallel.py:300-327). At most
+        the last _fin_cap episodes between two reads are kept."""
+        n = int(self._fin_n)
+        if n > self._fin_read:
+            lo = max(self._fin_read, n - self._fin_cap)
+            idx = torch.arange(lo, n, device=self.dev) % self._fin_cap
+            vals = self._fin[:, idx].cpu()
+            self._fin_host.append((vals[0], vals[1]))
+            self._fin_read = n
+        return self._fin_host
 
     # ------------------------------------------------------------------ observation
     def _observe(self) -> torch.Tensor:
@@ -210,7 +231,11 @@ class BatchedEnv:
                 info["terminal_obs"] = obs.clone()
             info["episode_return"] = self.episode_return.clone()
             info["episode_length"] = self.t.clone()
-            self.finished_returns.append((self.episode_return[done].cpu(), self.t[done].cpu()))
+            pos = self._fin_n + torch.cumsum(done, 0) - 1
+            slot = torch.where(done, pos % self._fin_cap, torch.full_like(pos, self._fin_cap))
+            self._fin[0].index_copy_(0, slot, self.episode_return)   # duplicates only into the sink
+            self._fin[1].index_copy_(0, slot, self.t)
+            self._fin_n += done.sum()
             if self.auto_reset:
                 self.reset(done)
         return self.obs, reward.to(torch.float32), done, info

@@ -69,6 +69,7 @@ def test_batched_env_cartpole_semantics():
     assert torch.allclose(env.t, torch.full_like(env.t, ph.control_interval * ph.dt))
     push = torch.full((16,), 20, dtype=torch.int32, device="cuda")   # full force: the pole falls
     done_seen = torch.zeros(16, dtype=torch.bool, device="cuda")
+    n_done, rets, lens = 0, [], []
     for _ in range(40):
         last = env.obs.clone()
         obs, rew, done, info = env.step(push)
@@ -77,8 +78,18 @@ def test_batched_env_cartpole_semantics():
         assert torch.all((rew == 1) | (rew == -1))
         assert torch.equal(rew == -1, done)
         done_seen |= done
+        if bool(done.any()):
+            n_done += int(done.sum())
+            rets.append(info["episode_return"][done].cpu())
+            lens.append(info["episode_length"][done].cpu())
     assert bool(done_seen.all())
-    assert len(env.finished_returns) > 0
+    # the device-compacted finished episodes: every one, in env order per step
+    fr = env.finished_returns
+    got_r = torch.cat([r for r, _ in fr])
+    got_l = torch.cat([t for _, t in fr])
+    assert got_r.numel() == n_done
+    assert torch.equal(got_r, torch.cat(rets)) and torch.equal(got_l, torch.cat(lens))
+    assert env.finished_returns is fr and sum(r.numel() for r, _ in fr) == n_done   # a second read adds nothing
 
 
 def test_batched_env_iqo_and_cooling_run():

@@ -64,6 +64,31 @@ __device__ __forceinline__ double dot_acc(double s, bool first, cx<RT> a, cx<RT>
         return first ? p : s + p;
     }
 }
+// A lane's partial Re<a, b> over its rows: fp64 exactly dot_acc's FMA chain; fp32 (C5) products summed
+// in fp32 within groups of 4 rows and each group added in fp64 (one convert + fp64 add per 4 rows
+// instead of per row; the group sums carry ~4 ulp of fp32, below the fp32 state's own rounding)
+template <typename RT>
+struct RowDot {
+    double s = 0.0;
+    RT g = RT(0);
+    int n = 0;
+    __device__ __forceinline__ void add(bool first, cx<RT> a, cx<RT> b) {
+        if constexpr (sizeof(RT) == 8) {
+            s = dot_acc(s, first, a, b);
+        } else {
+            g = a.re * b.re + (a.im * b.im + g);
+            if (++n == 4) {
+                s += (double)g;
+                g = RT(0);
+                n = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ double sum() const {
+        if constexpr (sizeof(RT) == 8) return s;
+        else return n ? s + (double)g : s;
+    }
+};
 // Factor-block reads: one buffer descriptor per slot block (SGPRs), per-lane VGPR offset, constant
 // SGPR / immediate byte offsets. Out-of-range reads return 0 (descriptor bounds = block size).
 using rsrc_t = __amdgpu_buffer_rsrc_t;
@@ -1120,12 +1145,13 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             }
             apply_x<FAM, R>(Ym, xYm, cf, lane);
             apply_x<FAM, R>(psi, xYp, cf, lane);
-            double sm[2] = {0.0, 0.0};
+            RowDot<RT> q0, q1;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                sm[0] = dot_acc(sm[0], j == 0, psi[j], xYp[j]);
-                sm[1] = dot_acc(sm[1], j == 0, Ym[j], xYm[j]);
+                q0.add(j == 0, psi[j], xYp[j]);
+                q1.add(j == 0, Ym[j], xYm[j]);
             }
+            double sm[2] = {q0.sum(), q1.sum()};
             step_sum<2>(sm);
             yp = a.w * sm[0];
             ym = a.w * sm[1];
@@ -1163,12 +1189,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             QC_STAMP(5);
             // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
             //   pp/pm = yp +- w kP (<Y+, X rel+> + <rel+, X Y+>) + w kP^2 <rel+, X rel+>
-            double d2[2] = {0.0, 0.0};
+            RowDot<RT> q0, q1;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                d2[0] = dot_acc(dot_acc(d2[0], j == 0, psi[j], xrp[j]), false, rp[j], xYp[j]);
-                d2[1] = dot_acc(d2[1], j == 0, rp[j], xrp[j]);
+                q0.add(j == 0, psi[j], xrp[j]);
+                q0.add(false, rp[j], xYp[j]);
+                q1.add(j == 0, rp[j], xrp[j]);
             }
+            double d2[2] = {q0.sum(), q1.sum()};
             step_sum<2>(d2);
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
@@ -1198,12 +1226,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 // whole (rows >= N are zero padding)
                 const int r0 = N - a.bnd_len, lt = r0 / R, jt = r0 - lt * R;
                 double suf = 0.0;
+                RowDot<RT> qx;
 #pragma unroll
                 for (int j = R - 1; j >= 0; --j) {
                     s[0] = dot_acc(s[0], j == R - 1, acc[j], acc[j]);
-                    s[1] = dot_acc(s[1], j == R - 1, acc[j], xn[j]);
+                    qx.add(j == R - 1, acc[j], xn[j]);
                     if (j == jt) suf = s[0];
                 }
+                s[1] = qx.sum();
                 stop = readlane_d(suf, lt);
                 for (int l = lt + 1; l <= (N - 1) / R; ++l) stop += readlane_d(s[0], l);
             } else {

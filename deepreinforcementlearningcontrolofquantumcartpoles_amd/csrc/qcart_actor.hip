@@ -376,15 +376,24 @@ __global__ __launch_bounds__(256) void k_mconv(const float* __restrict__ X, int 
     float xa[kQ][NT], wa[kQ][MT], xb[kQ][NT], wb[kQ][MT];
     fetch(0, xa, wa);
     int s = 0;
-    // sched_barriers pin the order: the next batch's loads are issued before this batch's MFMAs
+    // the next batch's loads interleaved one by one with this batch's MFMAs (sched_group_barrier:
+    // VMEM read 0x020, MFMA 0x008), so the load issue never holds the MFMA stream back
+    constexpr int NLD = kQ * (NT + MT), NMF = kQ * MT * NT;
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < (NLD > NMF ? NLD : NMF); ++i) {
+            if (i < NLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            if (i < NMF) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+    };
     for (; s + 2 * kQ <= STEPS; s += 2 * kQ) {
         fetch(s + kQ, xb, wb);
-        __builtin_amdgcn_sched_barrier(0);
         mma(kQ, xa, wa);
+        interleave();
         __builtin_amdgcn_sched_barrier(0);
         fetch(s + 2 * kQ, xa, wa);
-        __builtin_amdgcn_sched_barrier(0);
         mma(kQ, xb, wb);
+        interleave();
         __builtin_amdgcn_sched_barrier(0);
     }
     if (s + kQ <= STEPS) {   // one full batch (in xa) and a partial one

@@ -4,7 +4,7 @@ PKG := deepreinforcementlearningcontrolofquantumcartpoles_amd
 CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
-OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o)
+OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o)
 HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
 all: $(LIB) oracle

@@ -16,6 +16,7 @@ QC_HO, QC_IHO, QC_QO, QC_IQO = 0, 1, 2, 3
 QC_A_REFERENCE, QC_A_EXACT = 0, 1
 QC_RESET_GROUND, QC_RESET_RANDOM, QC_RESET_GAUSSIAN = 0, 1, 2
 QC_CTL_LQG, QC_CTL_DAMPING, QC_CTL_SEMICLASSICAL = 0, 1, 2
+QC_NOISE_PHILOX, QC_NOISE_MT19937 = 0, 1
 CONTROL_STRATEGIES = {"LQG": QC_CTL_LQG, "damping": QC_CTL_DAMPING, "semiclassical": QC_CTL_SEMICLASSICAL}
 
 STATUS = {
@@ -27,6 +28,7 @@ STATUS = {
 EXPORTS = (
     "qc_create", "qc_destroy", "qc_last_error", "qc_abi_version", "qc_get_params", "qc_dim", "qc_n_obs",
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
+    "qc_env_counters", "qc_set_seed_mt19937", "qc_noise_mode", "qc_mt19937_state", "qc_mt19937_words",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
     "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_record_row_len", "qc_record",
     "qc_scan_levels",
@@ -164,6 +166,11 @@ def lib() -> ctypes.CDLL:
     L.qc_set_step_counter.argtypes = [vp, u64]
     L.qc_get_step_counter.argtypes = [vp]
     L.qc_get_step_counter.restype = u64
+    L.qc_env_counters.argtypes = [vp, vp, vp]
+    L.qc_set_seed_mt19937.argtypes = [vp, vp]
+    L.qc_noise_mode.argtypes = [vp]
+    L.qc_mt19937_state.argtypes = [vp, vp, vp]
+    L.qc_mt19937_words.argtypes = []
     L.qc_set_dynamics.argtypes = [vp, d, d]
     L.qc_add_force.argtypes = [vp, d]
     L.qc_step.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp]

@@ -93,15 +93,62 @@ class Stepper:
         return torch.zeros((self.batch, self.N), dtype=self.state_dtype, device=self.device)
 
     def set_seed(self, seed: int):
+        """Philox noise keyed by seed, every env's counter back to 0 (qc_set_seed)."""
         L.check(L.lib().qc_set_seed(self._h, seed), self._h)
+
+    def set_seed_mt19937(self, seeds):
+        """The reference's noise stream (qc_set_seed_mt19937): env e draws from MT19937 seeded like
+        vslNewStream(VSL_BRNG_MT19937, seeds[e]) with MKL's Box-Muller transform. seeds: an int (every
+        env) or a sequence / tensor of B uint32 values."""
+        if isinstance(seeds, int):
+            seeds = [seeds] * self.batch
+        t = torch.as_tensor(seeds, dtype=torch.int64)
+        if t.shape != (self.batch,):
+            raise ValueError(f"seeds must have shape ({self.batch},)")
+        t = (t & 0xFFFFFFFF).to(torch.int64)
+        # uint32 bit patterns in an int32 tensor (torch has no uint32 arithmetic on every backend)
+        t = torch.where(t >= 2 ** 31, t - 2 ** 32, t).to(torch.int32).to(self.device).contiguous()
+        self._bind_stream()
+        L.check(L.lib().qc_set_seed_mt19937(self._h, _ptr(t)), self._h)
+        torch.cuda.current_stream(self.device).synchronize()
+
+    @property
+    def noise_mode(self) -> str:
+        return "mt19937" if L.lib().qc_noise_mode(self._h) == L.QC_NOISE_MT19937 else "philox"
 
     @property
     def step_counter(self) -> int:
+        """env 0's Philox counter (every env keeps its own: env_counters)."""
+        self._bind_stream()
         return int(L.lib().qc_get_step_counter(self._h))
 
     @step_counter.setter
     def step_counter(self, v: int):
+        self._bind_stream()
         L.check(L.lib().qc_set_step_counter(self._h, int(v)), self._h)
+
+    def env_counters(self, new: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Per-env Philox counters (int64 [B] copy); new replaces them (checkpoint / resume)."""
+        out = torch.empty((self.batch,), dtype=torch.int64, device=self.device)
+        if new is not None:
+            new = new.to(device=self.device, dtype=torch.int64).contiguous()
+            if new.shape != (self.batch,):
+                raise ValueError(f"counters must have shape ({self.batch},)")
+        self._bind_stream()
+        L.check(L.lib().qc_env_counters(self._h, _ptr(out), _ptr(new)), self._h)
+        return out
+
+    def mt19937_state(self, new: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Per-env MT19937 states (int32 [B][qc_mt19937_words] copy of the uint32 words); new replaces them."""
+        W = L.lib().qc_mt19937_words()
+        out = torch.empty((self.batch, W), dtype=torch.int32, device=self.device)
+        if new is not None:
+            new = new.to(device=self.device, dtype=torch.int32).contiguous()
+            if new.shape != (self.batch, W):
+                raise ValueError(f"state must have shape ({self.batch}, {W})")
+        self._bind_stream()
+        L.check(L.lib().qc_mt19937_state(self._h, _ptr(out), _ptr(new)), self._h)
+        return out
 
     def set_dynamics(self, dt: float, gamma: float):
         L.check(L.lib().qc_set_dynamics(self._h, dt, gamma), self._h)

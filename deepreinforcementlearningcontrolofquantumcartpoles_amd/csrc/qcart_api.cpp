@@ -39,8 +39,14 @@ struct qc_handle {
     bool mirror = false;
     OpHost op;
     std::vector<ActHost> acts;
-    uint64_t step = 0;
     std::string err;
+    // noise: per-env Philox counters [B] (always allocated); MT19937 mode: per-env states + the
+    // call's normals buffer
+    uint64_t* d_ctr = nullptr;
+    int noise_mode = QC_NOISE_PHILOX;
+    uint32_t* d_mt = nullptr;
+    double* d_noise = nullptr;
+    size_t noise_cap = 0;
     // device buffers
     double *d_xu = nullptr, *d_xg = nullptr, *d_hu = nullptr;
     double *d_tab = nullptr, *d_force = nullptr;
@@ -100,6 +106,9 @@ void free_dev(qc_handle* h) {
     if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
     if (h->d_order) { (void)hipFree(h->d_order); h->d_order = nullptr; h->order_cap = 0; }
     if (h->d_kb) { (void)hipFree(h->d_kb); h->d_kb = nullptr; }
+    if (h->d_ctr) { (void)hipFree(h->d_ctr); h->d_ctr = nullptr; }
+    if (h->d_mt) { (void)hipFree(h->d_mt); h->d_mt = nullptr; }
+    if (h->d_noise) { (void)hipFree(h->d_noise); h->d_noise = nullptr; h->noise_cap = 0; }
 }
 
 template <typename T>
@@ -184,7 +193,7 @@ KArgs base_args(const qc_handle* h) {
     a.B = p.batch;
     a.env_offset = p.env_offset;
     a.seed = p.seed;
-    a.step0 = h->step;
+    a.ctr = h->d_ctr;
     a.N = op.N;
     a.Npad = op.Npad;
     a.n_slots = (int32_t)h->acts.size();
@@ -328,6 +337,16 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
         delete h;
         return rc;
     }
+    {
+        std::vector<uint64_t> zero((size_t)std::max<int64_t>(p->batch, 1), 0);
+        rc = upload(h, &h->d_ctr, zero.data(), zero.size());
+    }
+    if (rc) {
+        set_create_err(h->err);
+        free_dev(h);
+        delete h;
+        return rc;
+    }
     *out = h;
     return QC_OK;
 }
@@ -372,15 +391,61 @@ int qc_sync(qc_handle* h) {
 int qc_set_seed(qc_handle* h, uint64_t seed) {
     if (!h) return QC_EINVAL;
     h->p.seed = seed;
-    h->step = 0;
-    return QC_OK;
+    h->noise_mode = QC_NOISE_PHILOX;
+    return qc_set_step_counter(h, 0);
 }
 int qc_set_step_counter(qc_handle* h, uint64_t step) {
     if (!h) return QC_EINVAL;
-    h->step = step;
+    DeviceGuard g(h->device);
+    if (launch_fill_u64(h->d_ctr, h->p.batch, step, h->stream)) return fail(h, QC_EHIP, "fill kernel launch failed");
     return QC_OK;
 }
-uint64_t qc_get_step_counter(const qc_handle* h) { return h ? h->step : 0; }
+uint64_t qc_get_step_counter(const qc_handle* h) {
+    if (!h || h->p.batch <= 0) return 0;
+    DeviceGuard g(h->device);
+    uint64_t v = 0;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return 0;
+    if (hipMemcpy(&v, h->d_ctr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v;
+}
+int qc_env_counters(qc_handle* h, uint64_t* out, const uint64_t* in) {
+    if (!h) return QC_EINVAL;
+    if (h->p.batch == 0) return QC_OK;
+    DeviceGuard g(h->device);
+    const size_t bytes = (size_t)h->p.batch * sizeof(uint64_t);
+    if (out && hip_check(h, hipMemcpyAsync(out, h->d_ctr, bytes, hipMemcpyDeviceToDevice, h->stream), "hipMemcpyAsync"))
+        return QC_EHIP;
+    if (in && hip_check(h, hipMemcpyAsync(h->d_ctr, in, bytes, hipMemcpyDeviceToDevice, h->stream), "hipMemcpyAsync"))
+        return QC_EHIP;
+    return QC_OK;
+}
+int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds) {
+    if (!h) return QC_EINVAL;
+    if (h->p.batch > 0 && !seeds) return fail(h, QC_EINVAL, "seeds is null");
+    DeviceGuard g(h->device);
+    if (h->p.batch > 0) {
+        if (!h->d_mt) {
+            hipError_t e = hipMalloc((void**)&h->d_mt, (size_t)h->p.batch * kMtWords * sizeof(uint32_t));
+            if (e != hipSuccess) { h->d_mt = nullptr; return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+        }
+        if (launch_mt_seed(seeds, h->p.batch, h->d_mt, h->stream)) return fail(h, QC_EHIP, "MT19937 seed kernel launch failed");
+    }
+    h->noise_mode = QC_NOISE_MT19937;
+    return QC_OK;
+}
+int qc_noise_mode(const qc_handle* h) { return h ? h->noise_mode : QC_EINVAL; }
+int qc_mt19937_state(qc_handle* h, uint32_t* out, const uint32_t* in) {
+    if (!h) return QC_EINVAL;
+    if (!h->d_mt) return fail(h, QC_EINVAL, "no MT19937 state (qc_set_seed_mt19937 first)");
+    DeviceGuard g(h->device);
+    const size_t bytes = (size_t)h->p.batch * kMtWords * sizeof(uint32_t);
+    if (out && hip_check(h, hipMemcpyAsync(out, h->d_mt, bytes, hipMemcpyDeviceToDevice, h->stream), "hipMemcpyAsync"))
+        return QC_EHIP;
+    if (in && hip_check(h, hipMemcpyAsync(h->d_mt, in, bytes, hipMemcpyDeviceToDevice, h->stream), "hipMemcpyAsync"))
+        return QC_EHIP;
+    return QC_OK;
+}
+int qc_mt19937_words(void) { return kMtWords; }
 
 int qc_set_dynamics(qc_handle* h, double dt, double gamma) {
     if (!h) return QC_EINVAL;
@@ -433,7 +498,6 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.env_steps = env_steps;
     a.default_action = default_action;
     a.n_steps = n_steps;
-    a.noise = noise;
     a.q_out = q_out;
     a.xm_out = xmean_out;
     a.fail_step = fail_step;
@@ -441,6 +505,23 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.obs_out = obs_out;
     DeviceGuard g(h->device);
     if (h->p.batch == 0) return QC_OK;
+    if (!noise && h->noise_mode == QC_NOISE_MT19937 && n_steps > 0) {
+        // the reference's stream: each env's MT19937 draws its steps' normals into the injected-noise
+        // buffer first (the state advances by exactly the words the env consumes)
+        const size_t need = (size_t)n_steps * (size_t)h->p.batch * 2;
+        if (h->noise_cap < need) {
+            if (h->d_noise) (void)hipFree(h->d_noise);
+            h->d_noise = nullptr;
+            h->noise_cap = 0;
+            hipError_t e = hipMalloc((void**)&h->d_noise, need * sizeof(double));
+            if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+            h->noise_cap = need;
+        }
+        if (launch_mt_normals(h->d_mt, h->p.batch, n_steps, env_steps, h->d_noise, h->stream))
+            return fail(h, QC_EHIP, "MT19937 normals kernel launch failed");
+        noise = h->d_noise;
+    }
+    a.noise = noise;
     if (actions || env_steps) {
         // group envs by force slot, padded to whole workgroups: every workgroup then shares one slot's
         // tables (the per-block LDS image); envs without a step budget form a last group of their own
@@ -464,7 +545,6 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     }
     int rc = launch_step(h->p.family, h->R, a, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
-    h->step += (uint64_t)n_steps;
     return QC_OK;
 }
 

@@ -44,7 +44,7 @@ struct KArgs {
     int64_t B;
     int64_t env_offset;
     uint64_t seed;
-    uint64_t step0;
+    uint64_t* ctr;             // [B] per-env noise counters: env e's Philox counter of its next step
     int32_t N;
     int32_t Npad;
     int32_t n_steps;
@@ -101,6 +101,14 @@ struct RecArgs {
     double scaling;
 };
 int launch_record(const RecArgs& a, void* stream);
+
+// reference noise stream (qcart_noise.hip): per-env MT19937 state [B][kMtWords] uint32 (624 words,
+// the read index, one pad word)
+constexpr int kMtWords = 626;
+int launch_mt_seed(const uint32_t* seeds, int64_t B, uint32_t* st, void* stream);
+int launch_mt_normals(uint32_t* st, int64_t B, int32_t n_steps, const int32_t* env_steps, double* noise,
+                      void* stream);
+int launch_fill_u64(uint64_t* p, int64_t n, uint64_t v, void* stream);
 
 // host-side launchers (qcart_kernels.hip)
 // (the kernel precision is a.precision)

@@ -1017,6 +1017,9 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         n_my = e < 0 ? 0 : (e < n_my ? e : n_my);
     }
     n_my = __builtin_amdgcn_readfirstlane(n_my);
+    // the env's own noise position: it advances by the steps this env takes, so an env's stream never
+    // depends on which other envs of the handle step in the same call (auto-reset, sharding)
+    const uint64_t ctr0 = a.ctr[env];
 #ifdef QCART_STAMPS
     unsigned long long st_acc[16] = {0}, st_t = 0;
     int st_ph = 9;
@@ -1032,7 +1035,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                     nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
                 }
             } else {
-                normals(a.seed, genv, a.step0 + (uint64_t)(k + lane), 0u, nz0, nz1);
+                normals(a.seed, genv, ctr0 + (uint64_t)(k + lane), 0u, nz0, nz1);
             }
         }
         const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
@@ -1292,6 +1295,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     if (lane == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;
+        a.ctr[env] = ctr0 + (uint64_t)n_my;
     }
     if (a.obs_out) {
         if constexpr (FAM <= 1) {

@@ -13,8 +13,11 @@ with the same function names, signatures, return values and error behaviour; eac
 kernels of libqcart (B = 1) and copies the numpy state to and from the device. This surface exists
 for drop-in compatibility; the throughput path is core.Stepper / env.BatchedEnv.
 
-Differences that cannot be pinned (documented in DESIGN.md): the noise is the counter-based Philox
-stream keyed by (seed, env 0, step) instead of MKL's MT19937.
+Noise: set_seed(seed) starts the reference's stream — MT19937 seeded like vslNewStream(VSL_BRNG_MT19937,
+seed), two Box-Muller normals per step (qc_set_seed_mt19937; MKL's uniform words bit for bit, its
+normals to <= 1 ulp of MKL's CBWR=COMPATIBLE path, tests/test_mkl_fixtures.py). Before the first
+set_seed the module, like the reference's, has no seeded stream; here it draws from seed 0's.
+load(..., noise="philox") selects the counter-based Philox stream instead.
 """
 from __future__ import annotations
 
@@ -43,13 +46,18 @@ def _check_state(state, N):
 class _Simulation:
     """One compiled-parameter set of the reference module (see load())."""
 
-    def __init__(self, physics: cfg.Physics, device: int = 0):
+    def __init__(self, physics: cfg.Physics, device: int = 0, noise: str = "mt19937"):
         import torch
 
         from .core import Stepper
+        if noise not in ("mt19937", "philox"):
+            raise ValueError("noise must be 'mt19937' or 'philox'")
         self._torch = torch
         self.physics = physics
+        self._noise = noise
         self._st = Stepper(physics, 1, device, seed=0)
+        if noise == "mt19937":
+            self._st.set_seed_mt19937(0)
         self._dev = self._st.device
         self._psi = self._st.new_state()
         self._dt, self._gamma = physics.dt, physics.gamma
@@ -59,7 +67,11 @@ class _Simulation:
     def set_seed(self, seed):
         if not isinstance(seed, (int, np.integer)):
             raise TypeError("seed must be an int")
-        self._st.set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
+        if self._noise == "mt19937":
+            # PyArg "i" then vslNewStream(..., MKL_UINT seed): the int's low 32 bits
+            self._st.set_seed_mt19937(int(seed) & 0xFFFFFFFF)
+        else:
+            self._st.set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
         return None
 
     # check_settings(): IHO/simulation_i.cpp:581-583 -> (n_max, omega); QO:652-654 -> (x_n, h, lambda, mass, moment)
@@ -127,18 +139,19 @@ class _Simulation:
         return None
 
 
-def load(family: int | str = cfg.IHO, device: int = 0, **params) -> types.ModuleType:
+def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", **params) -> types.ModuleType:
     """Return a module-like object equivalent to the reference's compiled `simulation` extension.
 
     family: 0/'harmonic', 1/'inverted_harmonic', 2/'quartic', 3/'inverted_quartic'; params are the
     setupC.py macros (n_max, omega / x_max, grid_size, lambda_, mass, moment_order) and optionally
-    gamma, time_steps, f_max, a_mode (defaults: the drivers' values, config.DEFAULTS)."""
+    gamma, time_steps, f_max, a_mode (defaults: the drivers' values, config.DEFAULTS). noise: 'mt19937'
+    (the reference's stream, default) or 'philox'."""
     if isinstance(family, str):
         family = {v: k for k, v in cfg.FAMILY_NAMES.items()}[family]
     phys = cfg.DEFAULTS[family].with_(**params)
-    key = (device, tuple(sorted(phys.asdict().items())))
+    key = (device, noise, tuple(sorted(phys.asdict().items())))
     if key not in _MODULES:
-        sim = _Simulation(phys, device)
+        sim = _Simulation(phys, device, noise)
         mod = types.ModuleType("simulation", "MI355X-native drop-in for the reference `simulation` module")
         for name in ("step", "simulate_10_steps", "set_seed", "check_settings", "x_expectation"):
             setattr(mod, name, getattr(sim, name))
@@ -149,10 +162,10 @@ def load(family: int | str = cfg.IHO, device: int = 0, **params) -> types.Module
     return _MODULES[key]
 
 
-def install(family: int | str = cfg.IHO, device: int = 0, **params) -> types.ModuleType:
+def install(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", **params) -> types.ModuleType:
     """Register the drop-in as `simulation` in sys.modules, so the reference drivers'
     `__import__('simulation')` resolves to it."""
-    mod = load(family, device, **params)
+    mod = load(family, device, noise, **params)
     sys.modules["simulation"] = mod
     return mod
 

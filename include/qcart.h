@@ -75,7 +75,7 @@ typedef struct qc_params {
                               Fock families; psi buffers are then complex64)                     */
     int64_t batch;         /* B envs held by this handle (this rank's shard)                   */
     int64_t env_offset;    /* global id of env 0 (multi-GPU sharding keeps noise invariant)    */
-    uint64_t seed;         /* Philox key (replaces set_seed's MT19937 stream, IHO:574-579)     */
+    uint64_t seed;         /* Philox key (QC_NOISE_PHILOX; MT19937: qc_set_seed_mt19937)       */
     double xth;            /* IQO per-step outside-probability window half-width (0 = off)      */
 } qc_params;
 
@@ -98,11 +98,38 @@ int qc_n_obs(const qc_handle* h);                /* 5 (Fock 'xp') or (2+m+1)*m/2
 int qc_set_stream(qc_handle* h, void* stream);
 int qc_sync(qc_handle* h);
 
-/* set_seed(int) (IHO/simulation_i.cpp:574-579): re-keys the counter-based noise and resets the
- * step counter. */
+/* Noise of the stochastic step (the two N(0,1) draws per go_one_step, IHO/simulation_i.cpp:435).
+ * Two sources, per handle:
+ *   QC_NOISE_PHILOX   (default) counter-based Philox4x32-10 keyed by (seed, env_offset + e); env e's
+ *                     counter is its own: it starts at 0 and advances by the steps env e takes, so an
+ *                     env's trajectory never depends on the other envs of the handle or on sharding.
+ *   QC_NOISE_MT19937  the reference's stream: set_seed(seed) = vslNewStream(VSL_BRNG_MT19937, seed) +
+ *                     vdRngGaussian(VSL_RNG_METHOD_GAUSSIAN_BOXMULLER) (IHO/simulation_i.cpp:574-579,
+ *                     :435), one stream per env (the reference runs one env per process with its own
+ *                     seed, IHO/main_parallel.py:173-178,358): init_by_array({seed}), two words per
+ *                     normal, x = sqrt(-2 ln u1) sin(2 pi u2), u = word * 2^-32 — MKL's uniform bits
+ *                     exactly and its Gaussians to <= 1 ulp of the MKL_CBWR=COMPATIBLE path
+ *                     (tests/golden/mkl_*.npz; MKL's default vector-math path differs by <= 5e-8).
+ * An injected `noise` array in qc_step overrides both and advances neither stream. */
+enum qc_noise_mode { QC_NOISE_PHILOX = 0, QC_NOISE_MT19937 = 1 };
+
+/* set_seed(int) (IHO/simulation_i.cpp:574-579), Philox mode: re-keys the counter-based noise and resets
+ * every env's counter to 0. */
 int qc_set_seed(qc_handle* h, uint64_t seed);
+/* set every env's Philox counter to `step` / read env 0's counter (synchronises) */
 int qc_set_step_counter(qc_handle* h, uint64_t step);
 uint64_t qc_get_step_counter(const qc_handle* h);
+/* per-env Philox counters (device uint64 [B]): copied to `out` and/or replaced from `in` (either may be
+ * NULL; checkpoint / resume of a batch) */
+int qc_env_counters(qc_handle* h, uint64_t* out, const uint64_t* in);
+/* set_seed for every env in MT19937 mode: seeds device uint32 [B], env e's stream
+ * vslNewStream(VSL_BRNG_MT19937, seeds[e]) */
+int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds);
+int qc_noise_mode(const qc_handle* h);
+/* per-env MT19937 states (device uint32 [B][qc_mt19937_words()]: 624 state words, read index, pad):
+ * copied to `out` and/or replaced from `in` */
+int qc_mt19937_state(qc_handle* h, uint32_t* out, const uint32_t* in);
+int qc_mt19937_words(void);
 
 /* Change dt / gamma (step()'s per-call arguments; reset_ab on dt change, IHO:377-383). */
 int qc_set_dynamics(qc_handle* h, double dt, double gamma);
@@ -120,8 +147,9 @@ int qc_add_force(qc_handle* h, double force);
  *             NULL -> every env uses `default_action`.
  *   env_steps [B] int32 per-env step budget: env e advances min(n_steps, env_steps[e]) steps (0 =
  *             frozen, e.g. a finished episode awaiting reset); NULL -> n_steps for every env.
- *   noise     [n_steps][B][2] fp64 N(0,1) draws to inject (parity tests), or NULL for the
- *             in-kernel Philox4x32-10 stream keyed by (seed, env_offset + e, step counter).
+ *   noise     [n_steps][B][2] fp64 N(0,1) draws to inject (parity tests), or NULL for the handle's
+ *             stream (qc_noise_mode: in-kernel Philox keyed by (seed, env_offset + e, env e's counter),
+ *             or env e's MT19937); only the first min(n_steps, env_steps[e]) steps of env e are read.
  *   q_out, xmean_out  [n_steps][B] per-step (q, x_mean) outputs of step(), or NULL.
  *   fail_step [B]: 1-based index of the first step after which Fail (check_boundary_error) held,
  *             0 if none; NULL to skip.
@@ -129,7 +157,7 @@ int qc_add_force(qc_handle* h, double force);
  *             states before each step and after the last: first k in [0, n_steps] with
  *             P_out > 0.5, -1 if none; requires params.xth > 0; NULL to skip.
  *   obs_out   [B][n_obs] fp64 observation of the final state (same as qc_moments), or NULL.
- * The step counter advances by n_steps.
+ * Env e's noise stream advances by the min(n_steps, env_steps[e]) steps it takes.
  */
 int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_action, int32_t n_steps,
             const int32_t* env_steps, const double* noise, double* q_out, double* xmean_out, int32_t* fail_step,

@@ -77,6 +77,13 @@ def lib():
         L.qo_tab_export.argtypes = [vp, vp, vp, vp]
         L.qo_philox4x32_10.argtypes = [vp, vp, vp]
         L.qo_normals.argtypes = [u64, u64, u64, vp]
+        L.qo_term7.argtypes = [vp, vp, vp, vp]
+        L.qo_tab_solve.argtypes = [vp, vp]
+        L.qo_grid_p_apply.argtypes = [vp, vp, d, vp]
+        L.qo_mt_seed.argtypes = [ctypes.c_uint32, vp]
+        L.qo_mt_next.argtypes = [vp]
+        L.qo_mt_next.restype = ctypes.c_uint32
+        L.qo_mt_normals.argtypes = [vp, i64, vp]
         L.qo_fock_random_state.argtypes = [vp, u64, u64, ctypes.c_int, vp]
         L.qo_gaussian_packet.argtypes = [vp, d, d, d, vp]
         L.qo_run_batch.argtypes = [vp, vp, i64, vp, d, ctypes.c_int, d, d, u64, i64, u64, vp, vp, vp,
@@ -179,6 +186,21 @@ class OracleSystem:
         lib().qo_tab_export(t, _ptr(ab), _ptr(ipiv), _ptr(A))
         return ab, ipiv, A
 
+    def term7(self, dt, force, v):
+        y = np.zeros(self.N, dtype=np.complex128)
+        lib().qo_term7(self._h, self.tab(dt, force), _ptr(np.ascontiguousarray(v, np.complex128)), _ptr(y))
+        return y
+
+    def tab_solve(self, dt, force, b):
+        x = np.ascontiguousarray(b, np.complex128).copy()
+        lib().qo_tab_solve(self.tab(dt, force), _ptr(x))
+        return x
+
+    def grid_p_apply(self, v, pbar):
+        y = np.zeros(self.N, dtype=np.complex128)
+        lib().qo_grid_p_apply(self._h, _ptr(np.ascontiguousarray(v, np.complex128)), pbar, _ptr(y))
+        return y
+
     def fock_random_state(self, seed, env_id, levels=16):
         psi = np.zeros(self.N, dtype=np.complex128)
         lib().qo_fock_random_state(self._h, seed, env_id, levels, _ptr(psi))
@@ -227,3 +249,25 @@ def philox(ctr, key):
     o = np.zeros(4, dtype=np.uint32)
     lib().qo_philox4x32_10(_ptr(c), _ptr(k), _ptr(o))
     return o
+
+
+class MT19937:
+    """The reference's noise stream restated (set_seed + vdRngGaussian BOXMULLER, IHO/simulation_i.cpp:
+    574-579, :435): MT19937 seeded by init_by_array({seed}), normals sqrt(-2 ln u1) sin(2 pi u2)."""
+
+    def __init__(self, seed: int):
+        self.st = np.zeros(625, dtype=np.uint32)
+        lib().qo_mt_seed(int(seed) & 0xFFFFFFFF, _ptr(self.st))
+
+    def words(self, n: int) -> np.ndarray:
+        return np.array([lib().qo_mt_next(_ptr(self.st)) for _ in range(n)], dtype=np.uint32)
+
+    def normals(self, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=np.float64)
+        lib().qo_mt_normals(_ptr(self.st), n, _ptr(out))
+        return out
+
+
+def mt_noise(seeds, n_steps: int) -> np.ndarray:
+    """[n_steps][B][2] normals of per-env MT19937 streams (the reference's 2 draws per step)."""
+    return np.stack([MT19937(s).normals(2 * n_steps).reshape(n_steps, 2) for s in seeds], axis=1)

@@ -541,6 +541,14 @@ static void sum_up(const qo_sys* s, const qo_tab* t, double* st, double dt, doub
 
 /* check_boundary_error: IHO/simulation_i.cpp:422-426 (5 top levels > 2e-3), HO/simulation.cpp:403-407
  * (> 1e-3), QO/simulation_quart.cpp:559-565 (6 points at either end > 5e-3) */
+/* exported pieces for the MKL-boundary fixtures (tests/test_mkl_fixtures.py) */
+void qo_term7(const qo_sys* s, const qo_tab* t, const double* v, double* y) {
+    term7_apply(s, t, (const zc*)v, (zc*)y);
+}
+void qo_tab_solve(const qo_tab* t, double* b) {
+    zgbtrs1(t->N, t->kl, t->kl, t->ab, t->ldab, t->ipiv, (zc*)b);
+}
+
 int qo_boundary_fail(const qo_sys* s, const double* psi_) {
     const zc* psi = (const zc*)psi_;
     const int N = s->N;
@@ -693,6 +701,10 @@ static void grid_p_apply(const qo_sys* s, const zc* v, double pbar, zc* out) {
 }
 
 /* compute_statistics: QO/simulation_quart.cpp:326-362 */
+void qo_grid_p_apply(const qo_sys* s, const double* v, double pbar, double* out) {
+    grid_p_apply(s, (const zc*)v, pbar, (zc*)out);
+}
+
 static void grid_moments(const qo_sys* s, const zc* psi, double* data) {
     const int N = s->N, m = s->p.moment_order;
     const double h = s->p.grid_size;
@@ -801,6 +813,55 @@ static void normals_tag(uint64_t seed, uint64_t env, uint64_t ctr_lo, uint32_t t
 }
 void qo_normals(uint64_t seed, uint64_t env_id, uint64_t step, double r[2]) {
     normals_tag(seed, env_id, step, 0u, r);
+}
+
+/* The reference's own stream (set_seed IHO/simulation_i.cpp:574-579, vdRngGaussian :435):
+ * VSL_BRNG_MT19937 = the Matsumoto-Nishimura mt19937ar generator seeded by init_by_array({seed}, 1);
+ * VSL_RNG_METHOD_GAUSSIAN_BOXMULLER: x = sqrt(-2 ln u1) sin(2 pi u2) from two consecutive outputs,
+ * u = word * 2^-32 (MKL documentation of the method; pinned bit for bit on the uniform words and to
+ * <= 1 ulp on the normals against MKL 2021.4 under MKL_CBWR=COMPATIBLE, tests/golden/mkl_stream.npz).
+ * State: st[0..623] words, st[624] read index (624 = twist before the next draw). */
+void qo_mt_seed(uint32_t seed, uint32_t* st) {
+    uint32_t* mt = st;
+    mt[0] = 19650218u;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    int i = 1, j = 0;
+    for (int k = 624; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + seed + (uint32_t)j;
+        i++; j++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+        if (j >= 1) j = 0;
+    }
+    for (int k = 623; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+    st[624] = 624;
+}
+uint32_t qo_mt_next(uint32_t* st) {
+    uint32_t* mt = st;
+    if (st[624] >= 624) {
+        for (int k = 0; k < 624; k++) {
+            uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+            mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        st[624] = 0;
+    }
+    uint32_t y = mt[st[624]++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+void qo_mt_normals(uint32_t* st, int64_t n, double* out) {
+    for (int64_t i = 0; i < n; i++) {
+        double u1 = (double)qo_mt_next(st) * 0x1.0p-32;
+        double u2 = (double)qo_mt_next(st) * 0x1.0p-32;
+        out[i] = sqrt(-2. * log(u1)) * sin(6.283185307179586 * u2);
+    }
 }
 
 /* synthetic Fock psi0: complex Gaussian coefficients on levels n < levels, normalised */

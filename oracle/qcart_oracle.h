@@ -67,9 +67,19 @@ void qo_dense_x(const qo_sys* s, double* out);
 int qo_tab_ldab(const qo_tab* t);
 void qo_tab_export(const qo_tab* t, double* ab_lu, int32_t* ipiv, double* a_band);
 
+/* MKL-boundary pieces (tests/test_mkl_fixtures.py): term7 = A . v under the a_mode semantics (IHO:551),
+ * the band solve in place (zgbtrs, IHO:487), the grid (p_hat - pbar I) v of compute_statistics (QO:337) */
+void qo_term7(const qo_sys* s, const qo_tab* t, const double* v, double* y);
+void qo_tab_solve(const qo_tab* t, double* b);
+void qo_grid_p_apply(const qo_sys* s, const double* v, double pbar, double* out);
+
 /* counter-based noise shared with the product: Philox4x32-10 */
 void qo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 void qo_normals(uint64_t seed, uint64_t env_id, uint64_t step, double r[2]);
+/* the reference's stream: MT19937 init_by_array({seed}) + MKL Box-Muller; st uint32 [625] */
+void qo_mt_seed(uint32_t seed, uint32_t* st);
+uint32_t qo_mt_next(uint32_t* st);
+void qo_mt_normals(uint32_t* st, int64_t n, double* out);
 void qo_fock_random_state(const qo_sys* s, uint64_t seed, uint64_t env_id, int levels, double* psi);
 void qo_gaussian_packet(const qo_sys* s, double wavenumber, double mean, double stdv, double* psi);
 

@@ -1,0 +1,173 @@
+"""GPU tests of the noise streams: the reference's MT19937 + Box-Muller stream on the device
+(qc_set_seed_mt19937), the drop-in reproducing the MKL-ordered reference trajectory from set_seed(seed)
+alone, and per-env Philox counters (an env's stream depends only on its own steps)."""
+from math import pi
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.env import BatchedEnv  # noqa: E402
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_v1.npz")
+
+
+def test_mt19937_states_and_trajectories_match_oracle(oracle_mod):
+    """Per-env MT19937 on the device: after a call with step budgets every env's state words equal the
+    oracle's stream advanced by exactly 4 words per step taken (bitwise), and the trajectories equal the
+    oracle fed the oracle's MT19937 normals (1e-12)."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=63)
+    seeds = [0, 1, 42, 99998, 4294967295]
+    B = len(seeds)
+    st = Stepper(ph, B, 0)
+    st.set_seed_mt19937(seeds)
+    assert st.noise_mode == "mt19937"
+    psi = st.new_state()
+    psi[:, 0] = 1.0
+    psi0 = psi.cpu().numpy()
+    budget = [170, 0, 100, 170, 5]      # 170 steps = 680 words: crosses a twist
+    acts = np.array([10, 12, 7, 9, 10], np.int32)
+    out = st.step(psi, torch.from_numpy(acts).cuda(), 170, env_steps=torch.tensor(budget, dtype=torch.int32,
+                                                                                   device="cuda"), want_q=True)
+    torch.cuda.synchronize()
+    W = 626
+    dev_state = st.mt19937_state().cpu().numpy().view(np.uint32).reshape(B, W)
+    osys = oracle_mod.OracleSystem(1, n_max=63)
+    for e, s in enumerate(seeds):
+        mt = oracle_mod.MT19937(s)
+        r = mt.normals(2 * budget[e]).reshape(budget[e], 1, 2)
+        assert np.array_equal(dev_state[e, :624], mt.st[:624]), e
+        assert dev_state[e, 624] == mt.st[624], e
+        ref = psi0[e:e + 1].copy()
+        if budget[e]:
+            osys.run_batch(ref, acts[e:e + 1], ph.f_max, budget[e], ph.dt, ph.gamma, noise=r, n_threads=1)
+        err = np.linalg.norm(psi[e].cpu().numpy() - ref[0])
+        assert err < 1e-12, (e, err)
+    # the next call continues each stream where it stopped
+    st.step(psi, torch.from_numpy(acts).cuda(), 3)
+    dev2 = st.mt19937_state().cpu().numpy().view(np.uint32).reshape(B, W)
+    for e, s in enumerate(seeds):
+        mt = oracle_mod.MT19937(s)
+        mt.words(4 * (budget[e] + 3))
+        assert np.array_equal(dev2[e, :625], mt.st), e
+
+
+@pytest.mark.parametrize("name", ["iho181", "iho512"])
+def test_dropin_set_seed_reproduces_mkl_reference_trajectory(name):
+    """The drop-in with the reference's call sequence — set_seed(seed), then step(state, dt, force,
+    gamma) 1000 times — equals the MKL-call-ordered stepper (tests/golden/mklref.py) on MKL's
+    CBWR=COMPATIBLE stream for that seed: psi to 1e-9 after 1000 steps, every step's q and x_mean to
+    1e-9, Fail never raised. Against MKL's default (AVX-512, reduced-accuracy normals) stream the
+    difference is bounded (< 1e-5) and reported, not a parity claim."""
+    with np.load(FIX) as z:
+        n_max = int(z[f"traj/{name}/n_max"])
+        dt, gamma, f_max = z[f"traj/{name}/phys"]
+        seed = int(z[f"traj/{name}/seed"])
+        acts = z[f"traj/{name}/actions"]
+        ref_q, ref_x = z[f"traj/{name}/cnr/q"], z[f"traj/{name}/cnr/x_mean"]
+        ref_psi, dflt_psi = z[f"traj/{name}/cnr/psi"], z[f"traj/{name}/default/psi"]
+    sim = S.load(cfg.IHO, n_max=n_max, time_steps=int(round(1 / dt)))
+    sim.set_seed(seed)
+    state = np.zeros(n_max + 1, np.complex128)
+    state[0] = 1.0
+    qs, xs, snaps = [], [], []
+    for k in range(len(ref_q)):
+        F = (int(acts[k // 80]) - 10) * (f_max / 10.)
+        q, xm, fail = sim.step(state, dt, F, gamma)
+        assert fail == 0
+        qs.append(q)
+        xs.append(xm)
+        if k + 1 in (100, 500, 1000):
+            snaps.append(state.copy())
+    assert np.abs(np.array(qs) - ref_q).max() < 1e-9
+    assert np.abs(np.array(xs) - ref_x).max() < 1e-9
+    errs = [np.linalg.norm(a - b) for a, b in zip(snaps, ref_psi)]
+    assert max(errs) < 1e-9, errs
+    d = np.linalg.norm(snaps[-1] - dflt_psi[-1])
+    print(f"{name}: |psi - psi_mkl_cnr| = {errs[-1]:.2e}, |psi - psi_mkl_default| = {d:.2e} after 1000 steps")
+    assert d < 1e-5
+
+
+def test_dropin_simulate_10_steps_matches_oracle(oracle_mod):
+    """simulate_10_steps (IHO/simulation_i.cpp:391-421): ten go_one_step calls, the LAST step's (q,
+    x_mean) and Fail of the final state only — against the oracle on the same MT19937 stream, up to and
+    including the call where the pushed pole first reaches the basis boundary (Fail = 1)."""
+    sim = S.load(cfg.IHO, n_max=31)
+    sim.set_seed(5)
+    o = oracle_mod.OracleSystem(1, n_max=31)
+    mt = oracle_mod.MT19937(5)
+    state = np.zeros(32, dtype=np.complex128)
+    state[0] = 1.0
+    ref = state.copy()
+    dt, gamma = 1 / 1440, 2 * pi
+    first_fail = None
+    for call in range(100):
+        force = 8.0 if call >= 5 else 0.8
+        q, xm, fail = sim.simulate_10_steps(state, dt, force, gamma)
+        for k in range(10):
+            q2, xm2, f2 = o.step(ref, dt, force, gamma, mt.normals(2))
+        assert abs(q - q2) < 1e-9 and abs(xm - xm2) < 1e-9, call
+        assert fail == f2, call                     # Fail of the final state, not "any step"
+        assert np.linalg.norm(state - ref) < 1e-9, call
+        if fail:
+            first_fail = call
+            break
+    assert first_fail is not None and first_fail > 5
+
+
+def test_per_env_counters_make_streams_independent():
+    """Philox noise keyed by each env's own counter: an env's trajectory depends only on the steps it
+    took, not on which other envs stepped in the same calls (the advisor's auto-reset finding)."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=63)
+    B = 6
+    st = Stepper(ph, B, 0, seed=13)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=8)
+    psi0 = psi.clone()
+    acts = torch.tensor([10, 11, 9, 10, 12, 8], dtype=torch.int32, device="cuda")
+    b1 = torch.tensor([80, 0, 40, 80, 0, 10], dtype=torch.int32, device="cuda")
+    st.step(psi, acts, 80, env_steps=b1)
+    st.step(psi, acts, 80)
+    assert st.env_counters().tolist() == [160, 80, 120, 160, 80, 90]
+    for e in range(B):   # the same calls on env e alone
+        one = Stepper(ph, 1, 0, seed=13, env_offset=e)
+        y = psi0[e:e + 1].clone()
+        one.step(y, acts[e:e + 1], 80, env_steps=b1[e:e + 1].clone())
+        one.step(y, acts[e:e + 1], 80)
+        torch.cuda.synchronize()
+        assert torch.equal(y[0], psi[e]), e
+    # checkpoint / resume of the counters
+    c = st.env_counters()
+    st.step_counter = 7
+    assert st.env_counters().tolist() == [7] * B
+    st.env_counters(c)
+    assert torch.equal(st.env_counters(), c)
+
+
+def test_batched_env_shards_equal_single_run_with_auto_reset():
+    """BatchedEnv with auto-reset: two shards (env_offset 0 and 4) reproduce a one-shard run bit for bit,
+    although the shards' episodes end (and restart) at different control steps."""
+    ph = cfg.DEFAULTS[cfg.IHO]
+    full = BatchedEnv(ph, 8, 0, seed=3)
+    halves = [BatchedEnv(ph, 4, 0, seed=3, env_offset=o) for o in (0, 4)]
+    full.reset()
+    for h in halves:
+        h.reset()
+    a = torch.tensor([20, 10, 10, 0, 10, 20, 11, 10], dtype=torch.int32, device="cuda")
+    n_done = 0
+    for _ in range(12):
+        _, _, d, _ = full.step(a)
+        n_done += int(d.sum())
+        for i, h in enumerate(halves):
+            h.step(a[4 * i:4 * i + 4])
+    torch.cuda.synchronize()
+    assert n_done > 0
+    assert torch.equal(full.psi[:4], halves[0].psi) and torch.equal(full.psi[4:], halves[1].psi)

@@ -58,6 +58,7 @@ class Stepper:
         self._h = h
         self.N = L.lib().qc_dim(h)
         self.n_obs = L.lib().qc_n_obs(h)
+        self.n_slots = physics.n_actions   # grows with add_force
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -154,7 +155,9 @@ class Stepper:
         L.check(L.lib().qc_set_dynamics(self._h, dt, gamma), self._h)
 
     def add_force(self, force: float) -> int:
-        return L.check(L.lib().qc_add_force(self._h, float(force)), self._h)
+        slot = L.check(L.lib().qc_add_force(self._h, float(force)), self._h)
+        self.n_slots = max(self.n_slots, slot + 1)
+        return slot
 
     def scan_levels(self, action: int):
         f, b = ctypes.c_int32(), ctypes.c_int32()
@@ -171,8 +174,7 @@ class Stepper:
         self._check_psi(psi)
         B = self.batch
         if actions is not None:
-            if actions.dtype != torch.int32 or actions.shape != (B,) or actions.device != self.device:
-                raise ValueError("actions must be an int32 tensor of shape (B,) on the handle's device")
+            self._check_actions(actions)
             actions = actions.contiguous()
         if default_action is None:
             default_action = self.physics.n_actions // 2
@@ -203,6 +205,25 @@ class Stepper:
             out["term_step"] = ts
         if want_obs:
             out["obs"] = ob
+        return out
+
+    def _check_actions(self, actions: torch.Tensor):
+        """int32 (B,) on the device, every value a valid slot (the reference's convert_to_force has no
+        other actions; an out-of-range one raises here instead of reaching the kernels)."""
+        if actions.dtype != torch.int32 or actions.shape != (self.batch,) or actions.device != self.device:
+            raise ValueError("actions must be an int32 tensor of shape (B,) on the handle's device")
+        if self.batch and bool(((actions < 0) | (actions >= self.n_slots)).any()):
+            raise ValueError(f"actions must lie in [0, {self.n_slots})")
+
+    def wavefunction_len(self) -> int:
+        return L.check(L.lib().qc_wavefunction_len(self._h), self._h)
+
+    def wavefunction_obs(self, psi: torch.Tensor, input_scaling: float = 1.0) -> torch.Tensor:
+        """get_data_wavefunction(state) * input_scaling (float32 [B][2 (N - 20)], qc_wavefunction_obs)."""
+        self._check_psi(psi)
+        out = torch.empty((self.batch, self.wavefunction_len()), dtype=torch.float32, device=self.device)
+        self._bind_stream()
+        L.check(L.lib().qc_wavefunction_obs(self._h, _ptr(psi), float(input_scaling), _ptr(out)), self._h)
         return out
 
     def moments(self, psi: torch.Tensor) -> torch.Tensor:

@@ -677,6 +677,7 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
     a.rows = rows;
     a.reward = reward;
     a.B = h->p.batch;
+    a.n_slots = (int32_t)h->acts.size();
     a.L = read_length;
     a.cg = coarse_grain;
     a.m = n_steps / coarse_grain;
@@ -688,6 +689,22 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
     DeviceGuard g(h->device);
     int rc = launch_record(a, h->stream);
     return rc ? fail(h, rc, "record kernel launch failed") : QC_OK;
+}
+
+int qc_wavefunction_len(const qc_handle* h) {
+    if (!h) return QC_EINVAL;
+    return 2 * (h->op.N - 20);   // Fock state[:-20], grid state[10:-10]
+}
+
+int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, float* out) {
+    if (!h) return QC_EINVAL;
+    if (h->p.batch > 0 && (!psi || !out)) return fail(h, QC_EINVAL, "psi and out are required");
+    if (h->op.N <= 20) return fail(h, QC_EINVAL, "the wavefunction input needs N > 20");
+    DeviceGuard g(h->device);
+    const int lo = h->op.fock ? 0 : 10;
+    int rc = launch_wavefunction(psi, h->p.precision, h->p.batch, h->op.N, lo, h->op.N - 20, input_scaling, out,
+                                 h->stream);
+    return rc ? fail(h, QC_EHIP, "wavefunction kernel launch failed") : QC_OK;
 }
 
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {

@@ -96,11 +96,14 @@ struct RecArgs {
     float* rows;                // [B][row_len] or null
     const float* reward;        // [B] or null
     int64_t B;
+    int32_t n_slots;            // action slots (out-of-range actions clamp like k_step's)
     int32_t L, m, K, cg, row_len;
     int32_t vec4;               // L, m multiples of 4: float4 history traffic
     double scaling;
 };
 int launch_record(const RecArgs& a, void* stream);
+int launch_wavefunction(const void* psi, int precision, int64_t B, int32_t N, int32_t lo, int32_t cnt, double scaling,
+                        float* out, void* stream);
 
 // reference noise stream (qcart_noise.hip): per-env MT19937 state [B][kMtWords] uint32 (624 words,
 // the read index, one pad word)

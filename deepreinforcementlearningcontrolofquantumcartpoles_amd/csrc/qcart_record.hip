@@ -43,7 +43,8 @@ __global__ __launch_bounds__(kRecThreads) void k_record(const RecArgs a) {
     }
     for (int j = tid; j < K + 1; j += kRecThreads) sf[j] = fresh ? 0.f : frc[j];
     __syncthreads();
-    const int slot = a.actions ? a.actions[env] : a.default_action;
+    int slot = a.actions ? a.actions[env] : a.default_action;
+    slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // as k_step (the host validates)
     const double f = a.slot_force[slot];
     const float fs = (float)(f * a.scaling);   // force * args.input_scaling (IHO:266, :288)
     const int64_t B = a.B;
@@ -99,7 +100,35 @@ __global__ __launch_bounds__(kRecThreads) void k_record(const RecArgs a) {
     }
 }
 
+// get_data_wavefunction (IHO/main_parallel.py:133-135: hstack(Re state[:-20], Im state[:-20]); IQO/QO
+// main_parallel.py:136-137: state[10:-10]) * input_scaling, in float32 like the reference's
+// float32 array times a Python float: out [B][2 * cnt]
+template <typename RT>
+__global__ __launch_bounds__(256) void k_wavefunction(const RT* psi, int64_t B, int32_t N, int32_t lo, int32_t cnt,
+                                                      float scaling, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * 2 * (int64_t)cnt) return;
+    const int64_t env = i / (2 * cnt);
+    const int j = (int)(i - env * 2 * cnt);
+    const int c = j >= cnt ? 1 : 0, r = lo + j - c * cnt;
+    out[i] = (float)psi[((size_t)env * N + r) * 2 + c] * scaling;
+}
+
 }  // namespace
+
+int launch_wavefunction(const void* psi, int precision, int64_t B, int32_t N, int32_t lo, int32_t cnt, double scaling,
+                        float* out, void* stream) {
+    const int64_t n = B * 2 * (int64_t)cnt;
+    if (n <= 0) return 0;
+    const dim3 g((unsigned)((n + 255) / 256));
+    if (precision == 1)
+        hipLaunchKernelGGL(k_wavefunction<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)psi, B, N, lo, cnt,
+                           (float)scaling, out);
+    else
+        hipLaunchKernelGGL(k_wavefunction<double>, g, dim3(256), 0, (hipStream_t)stream, (const double*)psi, B, N, lo,
+                           cnt, (float)scaling, out);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 int launch_record(const RecArgs& a, void* stream) {
     if (a.B <= 0) return 0;

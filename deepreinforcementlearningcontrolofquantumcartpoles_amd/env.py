@@ -16,7 +16,10 @@ Reference semantics reproduced per family ('xp' observation input):
         -phonon*scale (HO) / -energy*scale (QO) while phonon <= cutoff / energy < cutoff and no Fail;
         otherwise the episode ends without storing it; the episode is truncated at t_max = 100
 The experience row layout is the reference's: [last_obs, obs, last_action, reward]
-(IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged. With input='measurements'
+(IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged. With input='wavefunction'
+the observation is get_data_wavefunction(state) * input_scaling: float32 hstack(Re, Im) of state[:-20]
+(Fock, IHO/main_parallel.py:133-135) or state[10:-10] (grid, IQO/main_parallel.py:136-137)
+(qc_wavefunction_obs). With input='measurements'
 (HO, IHO; IHO/main_parallel.py:143-151,270-309) the observation is the device measurement record
 [B][2][read_length] (measurements.MeasurementRecord, updated in place by the qc_record kernel) and the
 experience rows [B][row_len] come from the same kernel (info['rows']).
@@ -58,8 +61,10 @@ class BatchedEnv:
         # no control at the zero-th step: the first decision follows one zero-force interval (IHO:250,
         # IQO:201, HO:238); QO decides at i = 0 (QO:208)
         self.first_interval = physics.family != cfg.QO
-        if input not in ("xp", "measurements"):
-            raise ValueError("input must be 'xp' or 'measurements'")
+        if input not in ("xp", "wavefunction", "measurements"):
+            raise ValueError("input must be 'xp', 'wavefunction' or 'measurements'")
+        if input == "measurements" and not physics.fock:
+            raise ValueError("the 'measurements' input exists for the Fock families (HO, IHO) only")
         self.input = input
         self.rec = None
         if input == "measurements":
@@ -70,8 +75,9 @@ class BatchedEnv:
         self.t = z(torch.float64)                 # episode time
         self.steps = z(torch.int64)               # physics steps in the episode
         self.last_action = torch.full((self.B,), self.half, dtype=torch.int32, device=self.dev)
+        obs_len = self.st.wavefunction_len() if input == "wavefunction" else self.st.n_obs
         self.obs = (self.rec.hist if self.rec is not None else
-                    torch.zeros((self.B, self.st.n_obs), dtype=torch.float32, device=self.dev))
+                    torch.zeros((self.B, obs_len), dtype=torch.float32, device=self.dev))
         self.episode_return = z(torch.float64)
         # finished episodes (return, length) compacted on the device into a ring of _fin_cap entries
         # (slot _fin_cap is the sink of the not-finished envs): no boolean indexing, no dynamic shapes and
@@ -96,8 +102,18 @@ class BatchedEnv:
             self._fin_read = n
         return self._fin_host
 
+    def _push_finished(self, done: torch.Tensor, ret: torch.Tensor, length: torch.Tensor):
+        """Append the finished episodes (env order) to the device ring, no host sync."""
+        pos = self._fin_n + torch.cumsum(done, 0) - 1
+        slot = torch.where(done, pos % self._fin_cap, torch.full_like(pos, self._fin_cap))
+        self._fin[0].index_copy_(0, slot, ret)   # duplicates only into the sink
+        self._fin[1].index_copy_(0, slot, length)
+        self._fin_n += done.sum()
+
     # ------------------------------------------------------------------ observation
     def _observe(self) -> torch.Tensor:
+        if self.input == "wavefunction":
+            return self.st.wavefunction_obs(self.psi, self.input_scaling)
         return self.st.moments(self.psi).to(torch.float32) * self.input_scaling
 
     def _quantity(self) -> torch.Tensor:
@@ -154,8 +170,9 @@ class BatchedEnv:
         self.last_action = torch.where(mask, torch.full_like(self.last_action, self.half), self.last_action)
         if self.first_interval:
             # no control at the zero-th step: one zero-force interval first (IHO:242-268, IQO:190-221,
-            # HO:237-257). An episode that already ends at i = control_interval stores nothing
-            # (i != control_interval guard, IHO:250) and is simply restarted here.
+            # HO:237-257). An episode that already ends at i = control_interval stores no transition
+            # (i != control_interval guard, IHO:250) but is still reported with its length t (the
+            # (experience, t, numerical_failure) / (t,) queue puts, IHO:312-313) and restarted here.
             fam = self.ph.family
             todo = mask.clone()
             while bool(todo.any()):
@@ -173,6 +190,8 @@ class BatchedEnv:
                     bad |= self.st.phonon_number(self.psi) > self.phonon_cutoff
                 bad &= todo
                 if bool(bad.any()):
+                    length = torch.where(mask, self.t + self.ci * self.ph.dt, self.t)
+                    self._push_finished(bad, torch.zeros_like(self.t), length)
                     self._reset_states(bad)
                 todo = bad
             self.t = torch.where(mask, self.t + self.ci * self.ph.dt, self.t)
@@ -231,11 +250,7 @@ class BatchedEnv:
                 info["terminal_obs"] = obs.clone()
             info["episode_return"] = self.episode_return.clone()
             info["episode_length"] = self.t.clone()
-            pos = self._fin_n + torch.cumsum(done, 0) - 1
-            slot = torch.where(done, pos % self._fin_cap, torch.full_like(pos, self._fin_cap))
-            self._fin[0].index_copy_(0, slot, self.episode_return)   # duplicates only into the sink
-            self._fin[1].index_copy_(0, slot, self.t)
-            self._fin_n += done.sum()
+            self._push_finished(done, self.episode_return, self.t)
             if self.auto_reset:
                 self.reset(done)
         return self.obs, reward.to(torch.float32), done, info

@@ -63,6 +63,7 @@ class MeasurementRecord:
             default_action = st.physics.n_actions // 2
         if actions is not None:
             actions = actions.to(device=st.device, dtype=torch.int32).contiguous()
+            st._check_actions(actions)
         if mode is not None:
             mode = mode.to(device=st.device, dtype=torch.uint8).contiguous()
         if reward is not None:

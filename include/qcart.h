@@ -183,6 +183,12 @@ int qc_energy(qc_handle* h, const void* psi, double* out);
 /* phonon_number(state) (HO/main_parallel.py:88-89, harmonic-cooling reward) = sum n |psi_n|^2: out [B] */
 int qc_phonon_number(qc_handle* h, const void* psi, double* out);
 
+/* get_data_wavefunction (args.input == 'wavefunction'): hstack(Re, Im) of state[:-20] (Fock,
+ * IHO/main_parallel.py:133-135) or state[10:-10] (grid, IQO/main_parallel.py:136-137), cast to float32 and
+ * times input_scaling in float32 (IHO:241,247): out [B][qc_wavefunction_len()] float32 (device) */
+int qc_wavefunction_len(const qc_handle* h);
+int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, float* out);
+
 /* Episode reset of psi for envs with mask[e] != 0 (mask NULL = all; device uint8 [B]):
  *   QC_RESET_GROUND   Fock |0> (IHO/main_parallel.py:231-232, HO/main_parallel.py:226-227)
  *   QC_RESET_RANDOM   Fock: normalised complex Gaussian amplitudes on levels < arg0 (synthetic

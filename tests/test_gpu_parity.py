@@ -127,12 +127,16 @@ def run_pair(oracle_mod, ph, steps, B, act_lo, act_hi, chunk=80, seed=7, policy=
 ])
 def test_psi_parity_injected_noise(oracle_mod, name, steps, B, policy):
     """||psi_GPU - psi_ref||_2 < 1e-9 after 1000 steps (fp64) for every env whose trajectory stays
-    physical (no boundary Fail); Fail steps themselves must agree. Under the PD policy the cartpole
-    stays up, so the 1000-step bound is exercised on (most of) the batch."""
-    worst, alive, _ = run_pair(oracle_mod, CASES[name], steps, B, 0, 20, policy=policy)
+    physical (no boundary Fail); Fail steps themselves must agree. Every case must keep at least half of
+    its envs physical to step 1000, so the 1000-step bound is never vacuous (random forces are drawn
+    from the middle 7 levels for the inverted oscillator, whose pole falls under full pushes; the PD
+    policy keeps it up from |0>)."""
+    ph = CASES[name]
+    lo, hi = (7, 13) if ph.family == cfg.IHO else (0, 20)
+    worst, alive, _ = run_pair(oracle_mod, ph, steps, B, lo, hi, policy=policy)
+    print(f"{name}: {int(alive.sum())}/{B} envs physical at step {steps}, max |dpsi| {worst:.2e}")
+    assert alive.sum() >= B // 2, f"only {int(alive.sum())}/{B} envs stayed physical to step {steps}"
     assert worst < TOL_1000, worst
-    if policy == "pd":
-        assert alive.sum() >= B // 2, "test setup: too few envs survived to step 1000"
 
 
 def test_psi_parity_inkernel_philox(oracle_mod):
@@ -348,10 +352,10 @@ def test_table_placements_bitwise_equal(monkeypatch, case):
     assert torch.equal(y[0], outs[0][5])
 
 
-@pytest.mark.parametrize("config", ["C2", "C4", "metric"])
+@pytest.mark.parametrize("config", ["C2", "C3", "C4", "metric"])
 def test_config_size_batch_properties(oracle_mod, config):
-    """At a BASELINE config's full per-GPU batch (C2: IHO N=512 B=4096; C4: IQO x_n=513, B=8192 per GPU
-    of its 8-GPU run; the metric: IHO N=512, B=65536 per GPU, the bench workload): every env stays
+    """At a BASELINE config's full per-GPU batch (C2: IHO N=512 B=4096; C3: QO x_n=1025, B=16384; C4: IQO
+    x_n=513, B=8192 per GPU of its 8-GPU run; the metric: IHO N=512, B=65536 per GPU, the bench workload): every env stays
     normalised, the call is deterministic, and sampled envs of the big batch match the oracle run alone
     with the same in-kernel Philox stream (1e-10 over 80 steps)."""
     conf = cfg.BENCH_CONFIGS[config]

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void k_copy(const CopyArgs a) {
 __global__ __launch_bounds__(256) void k_level(const State* st, const int64_t* leaf_slot, int64_t n_nodes,
                                                int64_t tree_size, double* tree, int up, int64_t n) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n || r >= st->n_leaf) return;
+    if (r >= n || r >= st->n_leaf || leaf_slot[r] < 0) return;   // < 0: a rejected update index
     int64_t node = n_nodes + leaf_slot[r];
     for (int u = 0; u < up; ++u) node = (node - 1) / 2;
     const int64_t cl = 2 * node + 1, cr = cl + 1;
@@ -293,8 +293,8 @@ struct UpdateArgs {
     const float* err;
     int32_t n;
     double* tree;
-    int64_t n_nodes;
-    int64_t* leaf_slot;   // out: the leaves to recompute (as slots)
+    int64_t n_nodes, cap;
+    int64_t* leaf_slot;   // out: the leaves to recompute (as slots; -1 = index rejected)
     float alpha, upper;
     double eps_scale;
 };
@@ -308,12 +308,15 @@ __global__ __launch_bounds__(kUpdThreads) void k_update(const UpdateArgs a) {
     float cm = 0.0f;
     for (int i = tid; i < a.n; i += kUpdThreads) {
         const float c = fminf(a.err[i] + eps, a.upper);   // np.minimum(abs_errors, abs_err_upper)
-        cm = fmaxf(cm, c);
         const int32_t ti = a.tree_idx[i];
+        // only leaf indices [n_nodes, n_nodes + capacity) are updates: anything else (an internal node, a
+        // stale or corrupt index) is skipped, so the tree and the device memory beyond it stay intact
+        const bool leaf = (int64_t)ti >= a.n_nodes && (int64_t)ti < a.n_nodes + a.cap;
+        if (leaf) cm = fmaxf(cm, c);
         bool last = true;
         for (int j = i + 1; j < a.n; ++j) last = last && a.tree_idx[j] != ti;
-        if (last) a.tree[ti] = (double)powf(c, a.alpha);   // np.power(clipped, alpha) in float32
-        a.leaf_slot[i] = (int64_t)ti - a.n_nodes;
+        if (leaf && last) a.tree[ti] = (double)powf(c, a.alpha);   // np.power(clipped, alpha) in float32
+        a.leaf_slot[i] = leaf ? (int64_t)ti - a.n_nodes : -1;
     }
     cmax[tid] = cm;
     __syncthreads();
@@ -589,6 +592,7 @@ int qc_replay_update(qc_replay* r, int32_t n, const int32_t* tree_idx, const flo
     ua.n = n;
     ua.tree = r->tree;
     ua.n_nodes = r->n_nodes;
+    ua.cap = r->p.capacity;
     ua.leaf_slot = r->leaf_slot;
     ua.alpha = (float)r->p.alpha;
     ua.upper = (float)r->p.abs_err_upper;

@@ -378,7 +378,8 @@ int qc_replay_store_xp(qc_replay* r, int64_t n, const uint8_t* valid, const floa
  * gather). Requires len >= 1 (the reference returns nothing while len < n). */
 int qc_replay_sample(qc_replay* r, int32_t n, const double* u, float* transitions, int32_t* tree_idx,
                      float* is_weights);
-/* Memory.batch_update (RL.py:438-446, :471-475): abs_errors [n] fp32 (the per-sample losses) */
+/* Memory.batch_update (RL.py:438-446, :471-475): abs_errors [n] fp32 (the per-sample losses); a tree_idx
+ * outside the leaves [n_nodes, n_nodes + capacity) is skipped (no write, no ancestor update) */
 int qc_replay_update(qc_replay* r, int32_t n, const int32_t* tree_idx, const float* abs_errors);
 /* Memory.clean / recalculate_structure (RL.py:312-331, :421-422): every parent recomputed */
 int qc_replay_rebuild(qc_replay* r);

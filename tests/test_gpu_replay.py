@@ -132,3 +132,32 @@ def test_passes_accumulate_like_the_reference(capacity, pbr, batches):
             if passes < 1.:
                 passes += inc
         assert dev.stats()["passes"] == passes, (n, dev.stats()["passes"], passes)
+
+
+def test_batch_update_skips_out_of_range_indices():
+    """batch_update indices outside the leaves [n_nodes, n_nodes + capacity) — an internal node, one past
+    the end, a negative one — are skipped: the tree is unchanged by them, valid indices in the same call
+    still update, and every parent stays left + right."""
+    cap, D = 100, 4
+    dev = PrioritizedReplay(cap, D, "sequential", device=0, seed=1)
+    orc = Memory(cap, D, "sequential", 0.0, seed=1)
+    rows = np.random.default_rng(0).normal(size=(60, D)).astype(np.float32)
+    dev.store(torch.from_numpy(rows).cuda())
+    for r in rows:
+        orc.store(r)
+    n_nodes = dev.stats()["n_nodes"]
+    good = np.array([n_nodes + 3, n_nodes + 10], np.int32)
+    bad = np.array([0, n_nodes - 1, n_nodes + cap, -5], np.int32)
+    err = np.array([0.5, 0.25, 0.9, 0.9, 0.9, 0.9], np.float32)
+    idx = np.concatenate([good, bad])
+    dev.batch_update(torch.from_numpy(idx).cuda(), torch.from_numpy(err).cuda())
+    orc.batch_update(good, err[:2])
+    tree, _ = dev.buffers()
+    tree = tree.cpu().numpy()
+    np.testing.assert_allclose(tree[n_nodes:], orc.tree.tree[n_nodes:], rtol=2e-7, atol=0)
+    assert dev.stats()["max"] == pytest.approx(orc.max, rel=1e-7)   # skipped errors do not raise max
+    par = np.arange(n_nodes)
+    l, r = 2 * par + 1, 2 * par + 2
+    n = len(tree)
+    np.testing.assert_array_equal(tree[par], np.where(l < n, tree[np.minimum(l, n - 1)], 0.)
+                                  + np.where(r < n, tree[np.minimum(r, n - 1)], 0.))

@@ -214,7 +214,10 @@ class BatchedEnv:
         out = self.st.step(self.psi, actions, self.ci, want_fail=True, want_obs=True,
                            want_term=(fam == cfg.IQO), want_q=self.rec is not None)
         fail = out["fail_step"] > 0
-        obs = out["obs"].to(torch.float32) * self.input_scaling
+        if self.input == "wavefunction":
+            obs = self.st.wavefunction_obs(self.psi, self.input_scaling)
+        else:
+            obs = out["obs"].to(torch.float32) * self.input_scaling
         self.t = self.t + self.ci * self.ph.dt
         self.steps = self.steps + self.ci
         if self.cartpole:

@@ -10,7 +10,11 @@ synthetic (random psi0 on Fock levels < 16, actions ~ U{0..20} redrawn every con
 resident in HBM before timing starts. value = physics env-steps/s over all ranks (one env-step =
 one reference simulation.step call). Multi-GPU: one process per GPU, env shard per rank
 (weak scaling, no data-path collective); RCCL all_reduce/all_gather only for the timing max and the
-episode-return gather after the timed region.
+episode-return gather after the timed region. `--gpus N` under torchrun (WORLD_SIZE set) runs this rank;
+without a launcher bench.py starts the N rank processes itself (before touching any GPU).
+The k_step time in `roofline` comes from HIP events the library records around each k_step launch on
+its stream (qc_set_timing); the CPU baseline runs the oracle in a child process on every usable host
+core (oracle/cpu_bench.py).
 """
 from __future__ import annotations
 
@@ -32,7 +36,8 @@ PEAK_FP32_VALU = 157.3e12  # MI355X FP32 vector (spec; config C5 computes in fp3
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without an external launcher bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="metric")
@@ -40,57 +45,43 @@ def parse():
     ap.add_argument("--sub-steps", type=int, default=0, help="physics steps per bench step (default: control interval)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every usable host core (affinity / cgroup quota)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: the ranks join a gloo group and report the world size")
     return ap.parse_args()
 
 
-def cpu_baseline(physics, seconds: float, threads: int):
-    """The oracle (CPU restatement of the reference scheme) on a bounded sample of the same workload."""
-    import numpy as np
-
-    from oracle import oracle as O
-    O.build()
-    s = O.OracleSystem(physics.family, n_max=physics.n_max, omega=physics.omega, x_max=physics.x_max,
-                       grid_size=physics.grid_size, lambda_=physics.lambda_, mass=physics.mass,
-                       moment_order=physics.moment_order, a_mode=physics.a_mode)
-    B = max(threads, 1) * 2
-    psi = np.stack([s.fock_random_state(1234, e, 16) for e in range(B)]) if physics.fock else None
-    if psi is None:
-        rng = np.random.default_rng(1)
-        psi = np.stack([s.gaussian_packet(rng.uniform(-.3, .3), rng.uniform(-1, 1), rng.uniform(.7, 1.3))
-                        for _ in range(B)])
-    acts = np.random.default_rng(0).integers(0, 21, B).astype(np.int32)
-    s.run_batch(psi, acts, physics.f_max, 5, physics.dt, physics.gamma, seed=42, n_threads=threads)  # warm
-    n = 0
-    t0 = time.perf_counter()
-    chunk = 20
-    while time.perf_counter() - t0 < seconds:
-        s.run_batch(psi, acts, physics.f_max, chunk, physics.dt, physics.gamma, seed=42, step0=n,
-                    n_threads=threads)
-        n += chunk
-    dtm = time.perf_counter() - t0
-    # single-core rate (one env on one thread, the reference's one-env-per-process model)
-    one = psi[:1].copy()
-    n1 = 0
-    t1 = time.perf_counter()
-    while time.perf_counter() - t1 < min(3.0, seconds / 4):
-        s.run_batch(one, acts[:1], physics.f_max, chunk, physics.dt, physics.gamma, seed=42, step0=n1, n_threads=1)
-        n1 += chunk
-    d1 = time.perf_counter() - t1
-    return {"value": B * n / dtm, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{B} envs x {n} physics steps (N={physics.dim}, fp64, OpenMP over envs, "
-                      f"one single-threaded env per thread), {dtm:.1f} s wall",
-            "single_core_value": n1 / d1, "cpu_model": _cpu_model()}
+def launch_ranks(n: int) -> int:
+    """--gpus N without WORLD_SIZE in the environment: start N copies of this script as ranks 0..N-1
+    (LOCAL_RANK = rank, one GPU each), before this process touches any GPU, and return the worst exit
+    code. Rank 0 prints the JSON line. The driver's torchrun launch sets WORLD_SIZE and skips this."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    return max(abs(p.wait()) for p in procs)
 
 
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return None
+def cpu_baseline(config: str, seconds: float, threads: int):
+    """The oracle (CPU restatement of the reference scheme) on a bounded sample of the same workload, in a
+    child process of its own (oracle/cpu_bench.py) so its OpenMP runtime starts with OMP_PROC_BIND=close
+    on every usable host core."""
+    import subprocess
+    env = dict(os.environ, OMP_PROC_BIND="close", OMP_PLACES="cores")
+    env.pop("OMP_NUM_THREADS", None)
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds)]
+    if threads:
+        cmd += ["--threads", str(threads)]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=seconds * 4 + 120)
+    if out.returncode != 0:
+        raise RuntimeError(out.stderr[-2000:])
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def latest_profile(workload: str):
@@ -107,17 +98,40 @@ def latest_profile(workload: str):
     return best
 
 
+def dry_run(world: int, rank: int):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size_seen": int(t.item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+        world = 1
+    elif world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(world, rank)
+
     import torch
     import torch.distributed as dist
 
     from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
     from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -143,7 +157,6 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(7 + rank)
     acts_all = torch.randint(0, ph.n_actions, (args.steps + args.warmup, B), generator=gen, device=dev,
                              dtype=torch.int32)
-    stream = torch.cuda.current_stream(dev)
 
     def one(k):
         return st.step(psi, acts_all[k], n_sub, want_fail=True, want_obs=True, want_term=(ph.family == 3))
@@ -154,21 +167,23 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    st.set_timing(True)          # HIP events around each k_step launch, on the stream it runs on
     t0 = time.perf_counter()
     for k in range(args.steps):
-        evs[k][0].record(stream)
         out = one(args.warmup + k)
-        evs[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_total, launches = st.step_kernel_time()
+    st.set_timing(False)
+    kern_ms = kern_total / max(launches, 1)
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    world_seen = 1
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        world_seen = dist.get_world_size()
         # RCCL gather of per-env episode statistics (here: survival flags of this control step)
         alive = (out["fail_step"] == 0).to(torch.float64).sum().reshape(1)
         gathered = [torch.zeros_like(alive) for _ in range(world)]
@@ -201,11 +216,16 @@ def main():
         "config": {"workload": f"{cfg.FAMILY_NAMES[ph.family]} N={N} per-GPU batch={B} "
                                f"{n_sub} physics steps + moments per step ({args.config})",
                    "global_batch": B * world, "seq_len": N, "parallelism": f"env-shard{world}",
-                   "physics_steps_per_step": n_sub},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM, "traffic": None,
-                     "kernel": "k_step", "kernel_ms": kern_ms,
-                     "note": f"achieved = {int(bpe)}*N B/env-step (psi read+write) x env-steps per launch / launch time"},
+                   "physics_steps_per_step": n_sub, "world_size_seen": world_seen},
+        # what bounds k_step is the FP vector pipe (psi stays in VGPRs across the fused steps); achieved /
+        # frac are the north-star yardstick: algorithmic psi bytes (read + write per physics step) / time
+        "roofline": {"bound": "fp32_valu" if fp32 else "fp64_valu", "achieved": achieved / 1e9,
+                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
+                     "yardstick": f"{int(bpe)}*N B/env-step (psi read+write) x env-steps per launch / k_step time "
+                                  "(SURVEY §8d north-star yardstick; the kernel keeps psi on chip, measured_gbs is "
+                                  "the real HBM traffic rate)",
+                     "kernel": "k_step", "kernel_ms": kern_ms, "kernel_launches": launches,
+                     "valu_frac": flops / peak_valu},
         "rl_steps_per_s": value / ph.control_interval,
         "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": peak_valu / 1e12,
                  "frac": flops / peak_valu, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
@@ -217,9 +237,10 @@ def main():
         res["roofline"]["traffic"] = prof["hbm_bytes_per_launch"]
         res["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC, profiles/%s_summary.json)" % prof["tag"]
         res["roofline"]["algorithmic_bytes_per_launch"] = bpe * N * per_launch_units
+        res["roofline"]["measured_gbs"] = prof["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(ph, args.cpu_seconds, args.cpu_threads)
+            res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds, args.cpu_threads)
         except Exception as e:  # the baseline is reported, never fatal
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

@@ -297,5 +297,16 @@ class Stepper:
         L.check(L.lib().qc_reset(self._h, _ptr(psi), kind, _ptr(mask), arg0, arg1, arg2, _ptr(k), _ptr(mean),
                                  _ptr(std)), self._h)
 
+    def set_timing(self, on: bool = True):
+        """HIP events around every k_step launch (qc_set_timing)."""
+        L.check(L.lib().qc_set_timing(self._h, int(bool(on))), self._h)
+
+    def step_kernel_time(self):
+        """(summed k_step ms, launches) since the last read (synchronises the stream)."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._bind_stream()
+        L.check(L.lib().qc_step_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), self._h)
+        return ms.value, n.value
+
     def sync(self):
         L.check(L.lib().qc_sync(self._h), self._h)

@@ -109,6 +109,9 @@ void free_dev(qc_handle* h) {
     if (h->d_ctr) { (void)hipFree(h->d_ctr); h->d_ctr = nullptr; }
     if (h->d_mt) { (void)hipFree(h->d_mt); h->d_mt = nullptr; }
     if (h->d_noise) { (void)hipFree(h->d_noise); h->d_noise = nullptr; h->noise_cap = 0; }
+    for (auto e : h->ev) (void)hipEventDestroy(e);
+    h->ev.clear();
+    h->ev_used = 0;
 }
 
 template <typename T>
@@ -543,8 +546,46 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         a.order = h->d_order;
         a.n_blocks = (uint32_t)(cap / W);
     }
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (h->timing) {
+        if (h->ev_used + 2 > h->ev.size()) {
+            for (int i = 0; i < 2; ++i) {
+                hipEvent_t e;
+                if (hipEventCreate(&e) != hipSuccess) return fail(h, QC_EHIP, "hipEventCreate failed");
+                h->ev.push_back(e);
+            }
+        }
+        ev0 = h->ev[h->ev_used];
+        ev1 = h->ev[h->ev_used + 1];
+        h->ev_used += 2;
+        (void)hipEventRecord(ev0, h->stream);
+    }
     int rc = launch_step(h->p.family, h->R, a, h->stream);
+    if (h->timing) (void)hipEventRecord(ev1, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
+    return QC_OK;
+}
+
+int qc_set_timing(qc_handle* h, int on) {
+    if (!h) return QC_EINVAL;
+    h->timing = on != 0;
+    h->ev_used = 0;
+    return QC_OK;
+}
+
+int qc_step_kernel_time(qc_handle* h, double* total_ms, int64_t* launches) {
+    if (!h) return QC_EINVAL;
+    DeviceGuard g(h->device);
+    if (hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize")) return QC_EHIP;
+    double tot = 0.0;
+    for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+        float ms = 0.f;
+        if (hip_check(h, hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]), "hipEventElapsedTime")) return QC_EHIP;
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (int64_t)(h->ev_used / 2);
+    h->ev_used = 0;
     return QC_OK;
 }
 

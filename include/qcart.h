@@ -163,6 +163,13 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             const int32_t* env_steps, const double* noise, double* q_out, double* xmean_out, int32_t* fail_step,
             int32_t* term_step, double* obs_out);
 
+/* Step-kernel timing (measurement, bench.py): with timing on, every qc_step records a HIP event pair on the
+ * handle's stream around its k_step launch only (not the grouping or noise kernels); qc_step_kernel_time
+ * synchronises the stream and returns the summed kernel time and the number of launches since the last
+ * call (then restarts the count). */
+int qc_set_timing(qc_handle* h, int on);
+int qc_step_kernel_time(qc_handle* h, double* total_ms, int64_t* launches);
+
 /* get_moments(state, out) (QO/simulation_quart.cpp:363-388) for grids; the Fock 'xp' vector
  * get_data_xp (IHO/main_parallel.py:129-131) for HO/IHO. out [B][n_obs] fp64. */
 int qc_moments(qc_handle* h, const void* psi, double* out);

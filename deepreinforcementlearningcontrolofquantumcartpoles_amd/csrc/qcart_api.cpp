@@ -47,6 +47,10 @@ struct qc_handle {
     uint32_t* d_mt = nullptr;
     double* d_noise = nullptr;
     size_t noise_cap = 0;
+    // step-kernel timing (qc_set_timing): a HIP event pair around every k_step launch on the handle's stream
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // [2 * n] start / stop
+    size_t ev_used = 0;
     // device buffers
     double *d_xu = nullptr, *d_xg = nullptr, *d_hu = nullptr;
     double *d_tab = nullptr, *d_force = nullptr;

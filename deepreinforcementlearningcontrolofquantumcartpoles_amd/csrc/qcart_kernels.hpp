@@ -423,6 +423,26 @@ __device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, 
     }
 }
 
+// grid H_F v row by row with the folded diagonal hfd_r = H_rr - cF x_r (X is diagonal on the grid):
+// f(j, (H_F v)_j.re, (H_F v)_j.im); padding rows (>= N) give 0
+template <int R, typename RT, typename F>
+__device__ __forceinline__ void grid_hf_rows(const cx<RT> (&v)[R], const RT (&hfd)[R], const Coef<2, R, RT>& cf, int lane,
+                                             F&& f) {
+    cx<RT> e[R + 8];
+    make_ext<R, 4>(v, e, lane);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        RT re = hfd[j] * v[j].re, im = hfd[j] * v[j].im;
+#pragma unroll
+        for (int d = 1; d <= 4; ++d) {
+            re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
+            im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
+        }
+        const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
+        f(j, in ? re : RT(0), in ? im : RT(0));
+    }
+}
+
 // H v and X v with one halo exchange
 template <int FAM, int R, typename RT>
 __device__ __forceinline__ void apply_hx(const cx<RT> (&v)[R], cx<RT> (&oh)[R], cx<RT> (&ox)[R], const Coef<FAM, R, RT>& cf,
@@ -732,6 +752,10 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
         }
     }
     QC_STAMP(11);
+    // pass 2 re-reads the factors through an opaque copy of the lane offset: at KL = 4 keeping pass 1's
+    // kl*R complex factors live across the scan instead costs 4 R complex registers per direction
+    Tab<MODE, RT> tb2 = tb;
+    if constexpr (KL == 4) asm volatile("" : "+v"(tb2.vc), "+v"(tb2.hc));
     // incoming state from lane - 1, pass 2
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
@@ -739,7 +763,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     for (int j = 0; j < R; ++j) {
         cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
+        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb2.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = y;
@@ -781,13 +805,15 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
         }
     }
     QC_STAMP(14);
+    Tab<MODE, RT> tb3 = tb;
+    if constexpr (KL == 4) asm volatile("" : "+v"(tb3.vc), "+v"(tb3.hc));
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
         cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb3.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -907,13 +933,16 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
 // waves (envs) per step workgroup: 8 (two per SIMD) where the step fits 256 VGPRs, else 4
+#ifndef QCART_W8_MAX_RG
+#define QCART_W8_MAX_RG 5
+#endif
 #ifndef QCART_W8_MAX_R
 #define QCART_W8_MAX_R 8
 #endif
 // (fp32 rows take half the registers: R_eff = R * sizeof(RT) / 8)
 template <int FAM, int R, typename RT = double>
 constexpr int kStepWaves =
-    ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= 5)) ? 8 : 4;
+    ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= QCART_W8_MAX_RG)) ? 8 : 4;
 
 template <int FAM, int R, int MODE, typename RT = double>
 __global__ __launch_bounds__((64 * kStepWaves<FAM, R, RT>))
@@ -987,15 +1016,23 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(RT(0), RT(0));
 
     const bool win_on = a.win_hi > a.win_lo;
-    cx<RT> xp[R];
-    apply_x<FAM, R>(psi, xp, cf, lane);
+    // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)
+    cx<RT> xp[FAM == 2 ? 1 : R];
+    if constexpr (FAM != 2) apply_x<FAM, R>(psi, xp, cf, lane);
+    // grid: H_F's diagonal with the slot's force folded in, once per call
+    RT hfd[FAM == 2 ? R : 1];
+    if constexpr (FAM == 2) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) hfd[j] = cf.hu[j] - cF * cf.xg[j];
+    }
     RT xbar;
     int term = -1, fail = 0;
     {
         double s[2] = {0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            s[0] += (double)(psi[j].re * xp[j].re + psi[j].im * xp[j].im);
+            if constexpr (FAM == 2) s[0] += (double)(cf.xg[j] * (psi[j].re * psi[j].re + psi[j].im * psi[j].im));
+            else s[0] += (double)(psi[j].re * xp[j].re + psi[j].im * xp[j].im);
             const int r = base + j;
             if (r >= a.win_lo && r < a.win_hi) s[1] += (double)(psi[j].re * psi[j].re + psi[j].im * psi[j].im);
         }
@@ -1055,6 +1092,138 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         const double c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
         const double c6 = 0.25 * sdt * dW;
 
+        if constexpr (FAM == 2) {
+            // Grid family (QO / IQO): X = diag(x_r), so every X product of the scheme is a per-row
+            // multiply — rel = (x - xbar) psi, X Y, X rel and the branch means are recomputed row by row
+            // instead of held — and H_F = H - cF X has the folded diagonal hfd. At most four R-row complex
+            // vectors are live (psi, D1, acc and the Horner temporary): R = 9 (C4, x_n = 513) fits two
+            // waves per SIMD and R = 17 (C3, x_n = 1025) one wave without spills. Same scheme as the Fock
+            // body below (go_one_step, QO/simulation_quart.cpp:569-624), term by term.
+            cx<RT> acc[R], D1[R];
+            auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
+                grid_hf_rows<R>(v, hfd, cf, lane, [&](int j, RT re, RT im) { u[j] = C(re, im); });
+            };
+            // A: D1 = -i H_F psi - g/4 (x - xbar)^2 psi   (D1, QO:434-459)
+            hf(psi, D1);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const RT xr = cf.xg[j] - xbar, q = g4r * xr * xr;
+                D1[j] = C(D1[j].im - q * psi[j].re, -D1[j].re - q * psi[j].im);
+            }
+            QC_STAMP(1);
+            // B: term7 = A D1 by Horner in H_F on A / a5 (QO:414-425, :631)
+            const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2), kY = (RT)(sdt * beta);
+            cx<RT> Ym[R];
+            {
+                cx<RT> t[R];
+                hf(D1, acc);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(-acc[j].im - b4r * D1[j].re, acc[j].re - b4r * D1[j].im);
+                hf(t, acc);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b3r * D1[j].im, acc[j].im - b3r * D1[j].re);
+                hf(t, acc);
+#pragma unroll
+                for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b2r * D1[j].re, acc[j].im + b2r * D1[j].im);
+                hf(t, acc);
+                hf(acc, t);
+                // acc = psi + kA rel + k2 D1 + a5 t; Y0 = psi + dt D1; Y-+ = Y0 -+ kY rel (Y+ in psi)
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const RT xr = cf.xg[j] - xbar;
+                    const cx<RT> rl = C(xr * psi[j].re, xr * psi[j].im);
+                    acc[j] = C(psi[j].re + kA * rl.re + k2 * D1[j].re + a5r * t[j].re,
+                               psi[j].im + kA * rl.im + k2 * D1[j].im + a5r * t[j].im);
+                    const cx<RT> y0 = C(psi[j].re + dtr * D1[j].re, psi[j].im + dtr * D1[j].im);
+                    Ym[j] = C(y0.re - kY * rl.re, y0.im - kY * rl.im);
+                    psi[j] = C(y0.re + kY * rl.re, y0.im + kY * rl.im);
+                }
+            }
+            QC_STAMP(3);
+            const RT kIm = (RT)(c1 - c6);
+            const double kP = sdt * beta;
+            double yp, ym;
+            {
+                // unnormalised means of Y+ and Y- (x |Y|^2 summed; D1ImRe QO:461-486)
+                double sm[2] = {0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    sm[0] += (double)(cf.xg[j] * (psi[j].re * psi[j].re + psi[j].im * psi[j].im));
+                    sm[1] += (double)(cf.xg[j] * (Ym[j].re * Ym[j].re + Ym[j].im * Ym[j].im));
+                }
+                step_sum<2>(sm);
+                yp = a.w * sm[0];
+                ym = a.w * sm[1];
+            }
+            {
+                // Y- branch: acc -= (c1 - c6) (-i H_F Y-); acc += (kRe x + kDm) rel-, rel- = (x - ym) Y-
+                const double kRed = -(c2 - c1) * g4;
+                const RT kRe = (RT)kRed, kDm = (RT)((c4 - c3 + c5) * beta - kRed * ym), ymr = (RT)ym;
+                grid_hf_rows<R>(Ym, hfd, cf, lane, [&](int j, RT hre, RT him) {
+                    const RT cr = (kRe * cf.xg[j] + kDm) * (cf.xg[j] - ymr);
+                    acc[j] = C(acc[j].re - kIm * him + cr * Ym[j].re, acc[j].im + kIm * hre + cr * Ym[j].im);
+                });
+            }
+            QC_STAMP(4);
+            {
+                // Y+ branch: acc += (c1 - c6) (-i H_F Y+); rel+ = (x - yp) Y+, and the Phi+- means from
+                // <Y+, X rel+> + <rel+, X Y+> = 2 x (x - yp) |Y+|^2 and <rel+, X rel+> = x (x - yp)^2 |Y+|^2
+                const RT ypr = (RT)yp;
+                double d2[2] = {0.0, 0.0};
+                grid_hf_rows<R>(psi, hfd, cf, lane, [&](int j, RT hre, RT him) {
+                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);
+                    const RT xr = cf.xg[j] - ypr, p2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+                    d2[0] += (double)(2 * cf.xg[j] * xr * p2);
+                    d2[1] += (double)(cf.xg[j] * xr * xr * p2);
+                });
+                step_sum<2>(d2);
+                QC_STAMP(6);
+                const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp, k5 = c5 * beta;
+                const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
+                // acc += fx X rel+ + fy Y+ + fr rel+ = (fx x (x - yp) + fy + fr (x - yp)) Y+
+                const RT fx = (RT)(kRed + 2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(kDpd - k5 * kP * spm);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const RT xr = cf.xg[j] - ypr, cr = (fx * cf.xg[j] + fr) * xr + fy;
+                    acc[j] = C(acc[j].re + cr * psi[j].re, acc[j].im + cr * psi[j].im);
+                }
+            }
+            QC_STAMP(7);
+            band_solve<KL, R, MODE, false>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
+            QC_STAMP(8);
+            {
+                // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
+                double s[2] = {0.0, 0.0}, pwin = 0.0, stop = 0.0, sbot = 0.0, ptop = 0.0, pbot = 0.0;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
+                    s[0] += p2;
+                    s[1] += (double)cf.xg[j] * p2;
+                    const int r = base + j;
+                    if (r >= N - a.bnd_len && r < N) ptop += p2;
+                    if (r < a.bnd_len) pbot += p2;
+                    if (r >= a.win_lo && r < a.win_hi) pwin += p2;
+                }
+                for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
+                for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
+                step_sum<2>(s);
+                double scale = __builtin_amdgcn_rsq(s[0]);
+                scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
+                scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
+                scale = scale * a.inv_sqrt_w;
+#pragma unroll
+                for (int j = 0; j < R; ++j) psi[j] = C(acc[j].re * (RT)scale, acc[j].im * (RT)scale);
+                xbar = (RT)(a.w * (s[1] * scale) * scale);
+                const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
+                const bool f = stop * sc2 > thr2 || sbot * sc2 > thr2;
+                if (f && fail == 0) fail = k + 1;
+                if (win_on && term < 0) {
+                    double sw[1] = {pwin};
+                    step_sum<1>(sw);
+                    if (1.0 - a.h * (sw[0] * scale) * scale > 0.5) term = k + 1;
+                }
+            }
+        } else {
         // Live vectors are kept to at most five R-row complex vectors (plus one halo) at any point so
         // the whole step fits 256 VGPRs: two waves per SIMD. Phases (go_one_step, IHO:432-489):
         //   A  rel = (X - xbar) psi, D1 = -i H_F psi - g/4 (X - xbar) rel          (D1: IHO:279-298)
@@ -1279,6 +1448,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 }
             }
         }
+        }   // Fock families
     }
 #ifdef QCART_STAMPS
     QC_STAMP(9);

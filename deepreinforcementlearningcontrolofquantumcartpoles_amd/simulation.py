@@ -95,28 +95,31 @@ class _Simulation:
             return a + half
         return self._st.add_force(float(force))
 
-    def _run(self, state, dt, force, gamma, n):
+    def _run(self, state, dt, force, gamma, n, final_fail: bool):
+        """n physics steps on the device; returns (q, x_mean, Fail) of the call (last step's q / x_mean;
+        Fail = any step's boundary test (step) or the final state's (simulate_10_steps)). One host->device
+        copy of the state and ONE device->host copy of state + the three scalars per call."""
         _check_state(state, self.N)
         self._sync_dynamics(float(dt), float(gamma))
         torch = self._torch
         self._psi.copy_(torch.from_numpy(state).view(1, -1))
         out = self._st.step(self._psi, None, n, default_action=self._slot(float(force)), want_q=True,
                             want_fail=True)
-        state[:] = self._psi.view(-1).cpu().numpy()
-        return out
+        fail = out["fail_step"]
+        if final_fail:
+            fail = self._st.boundary_fail(self._psi)
+        buf = torch.cat([self._psi.view(-1).view(torch.float64), out["q"][n - 1], out["x_mean"][n - 1],
+                         fail.to(torch.float64)]).cpu().numpy()
+        state[:] = buf[:2 * self.N].view(np.complex128)
+        return float(buf[2 * self.N]), float(buf[2 * self.N + 1]), int(buf[2 * self.N + 2] > 0)
 
     # step(state, dt, force, gamma) -> (q, x_mean, Fail): IHO/simulation_i.cpp:358-389
     def step(self, state, dt, force, gamma):
-        out = self._run(state, dt, force, gamma, 1)
-        q = float(out["q"][0, 0])
-        xm = float(out["x_mean"][0, 0])
-        return q, xm, int(out["fail_step"][0] > 0)
+        return self._run(state, dt, force, gamma, 1, False)
 
     # simulate_10_steps: IHO/simulation_i.cpp:391-421 (last step's q, x_mean; Fail of the final state)
     def simulate_10_steps(self, state, dt, force, gamma):
-        out = self._run(state, dt, force, gamma, 10)
-        fail = int(self._st.boundary_fail(self._psi)[0])
-        return float(out["q"][9, 0]), float(out["x_mean"][9, 0]), fail
+        return self._run(state, dt, force, gamma, 10, True)
 
     # x_expectation(state): IHO/simulation_i.cpp:204-215, QO/simulation_quart.cpp:244-258
     def x_expectation(self, state):

@@ -14,8 +14,9 @@ all: $(LIB) oracle
 KFLAGS ?= -mllvm -disable-machine-licm
 # (the grid TU keeps LICM: its 9-band loop-invariant addressing is worth hoisting, measured +12 %)
 $(CSRC)/build/qcart_k_grid.o: KFLAGS :=
-# fp32 TU: no SLP packing (v_pk_fma_f32 pairs cost more register shuffles than they save here)
-$(CSRC)/build/qcart_k_f32.o: KFLAGS += -fno-slp-vectorize
+# fp32 TU: complex values as packed 2-lane vectors (QCART_F32_PACKED, explicit v_pk_* arithmetic; MS property
+# accessors keep .re/.im) and no SLP packing of the remaining scalar code (it would reshuffle the pairs)
+$(CSRC)/build/qcart_k_f32.o: KFLAGS += -fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED
 $(CSRC)/build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c $< -o $@

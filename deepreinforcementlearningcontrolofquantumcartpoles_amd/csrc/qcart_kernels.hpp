@@ -29,26 +29,71 @@ template <typename RT>
 struct cx {
     RT re, im;
 };
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f splat(float k) { return (v2f){k, k}; }
+#ifdef QCART_F32_PACKED
+constexpr bool kPackedF32 = true;
+// fp32 (C5) complex values as one 2-lane vector in an aligned VGPR pair, so the complex products of the
+// banded solve and its scan (cmul / cmac / cmsub) issue as packed v_pk_fma_f32 / v_pk_mul_f32: two fp32
+// ops per lane per instruction. .re / .im stay usable as members (MS property accessors, -fms-extensions
+// in this translation unit only), so every scalar expression of the shared code compiles unchanged.
+// Measured (C5, same call): 58.7 -> 53.4 ms per launch. Packing the stencils, the step-body
+// combinations or the mirror as well raised the R = 32 kernel's spills (100 -> 200-380 registers) and
+// made it slower (63-137 ms): only the solve is packed.
+template <>
+struct cx<float> {
+    v2f v;
+    __device__ __forceinline__ float get_re() const { return v.x; }
+    __device__ __forceinline__ void put_re(float f) { v.x = f; }
+    __device__ __forceinline__ float get_im() const { return v.y; }
+    __device__ __forceinline__ void put_im(float f) { v.y = f; }
+    __declspec(property(get = get_re, put = put_re)) float re;
+    __declspec(property(get = get_im, put = put_im)) float im;
+};
+__device__ __forceinline__ cx<float> CV(v2f v) {
+    cx<float> c;
+    c.v = v;
+    return c;
+}
+#else
+constexpr bool kPackedF32 = false;
+__device__ __forceinline__ cx<float> CV(v2f v) { return cx<float>{v.x, v.y}; }   // (packed TU only)
+#endif
+// packed fp32 branch of a template on RT (compile-time; fp64 code is never affected)
+template <typename RT>
+constexpr bool kPk = kPackedF32 && sizeof(RT) == 4;
 using cd = cx<double>;
 template <typename RT>
 __device__ __forceinline__ cx<RT> C(RT r, RT i) {
     cx<RT> c;
+    if constexpr (kPk<RT>) {
+        c.v = (v2f){r, i};
+        return c;
+    }
     c.re = r;
     c.im = i;
     return c;
 }
 template <typename RT>
 __device__ __forceinline__ cx<RT> cmul(cx<RT> a, cx<RT> b) {
+    if constexpr (kPk<RT>)   // (a.re b.re - a.im b.im, a.re b.im + a.im b.re): 1 pk_mul + 1 pk_fma
+        return CV(__builtin_elementwise_fma((v2f){-a.v.y, a.v.y}, b.v.yx, splat(a.v.x) * b.v));
     return C(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
 }
 template <typename RT>
 __device__ __forceinline__ cx<RT> cmac(cx<RT> acc, cx<RT> a, cx<RT> b) {   // acc + a*b
+    if constexpr (kPk<RT>)
+        return CV(__builtin_elementwise_fma((v2f){-a.v.y, a.v.y}, b.v.yx,
+                                            __builtin_elementwise_fma(splat(a.v.x), b.v, acc.v)));
     return C(acc.re + a.re * b.re - a.im * b.im, acc.im + a.re * b.im + a.im * b.re);
 }
 // acc - a*b as two FMA chains (4 FP ops; acc - (a*b) as written would cost 6: contraction cannot
 // reassociate the inner difference)
 template <typename RT>
 __device__ __forceinline__ cx<RT> cmsub(cx<RT> acc, cx<RT> a, cx<RT> b) {
+    if constexpr (kPk<RT>)   // (acc.re + a.im b.im - a.re b.re, acc.im - a.im b.re - a.re b.im)
+        return CV(__builtin_elementwise_fma((v2f){a.v.y, -a.v.y}, b.v.yx,
+                                            __builtin_elementwise_fma(splat(-a.v.x), b.v, acc.v)));
     return C(acc.re + a.im * b.im - a.re * b.re, acc.im - a.im * b.re - a.re * b.im);
 }
 template <typename RT>

@@ -36,13 +36,14 @@ clean:
 
 .PHONY: all oracle clean resource-usage expt expt_actor
 
-# experiment builds (not shipped): make expt EXPT=-DQCART_EXPT_NOLOAD NAME=noload
+# experiment builds (not shipped): make expt EXPT=-DQCART_EXPT_NOLOAD NAME=noload [TU=qcart_k_grid]
 EXPT ?=
 NAME ?= expt
-expt:
+TU ?= qcart_k_iho
+expt: $(OBJS)
 	@mkdir -p $(CSRC)/build_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(EXPT) -c $(CSRC)/qcart_k_iho.hip -o $(CSRC)/build_$(NAME)/qcart_k_iho.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/qcart_k_iho.o $(filter-out $(CSRC)/build/qcart_k_iho.o,$(OBJS))
+	$(HIPCC) $(HIPFLAGS) $(if $(filter qcart_k_grid,$(TU)),,$(KFLAGS)) $(if $(filter qcart_k_f32,$(TU)),-fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED,) $(EXPT) -c $(CSRC)/$(TU).hip -o $(CSRC)/build_$(NAME)/$(TU).o
+	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/$(TU).o $(filter-out $(CSRC)/build/$(TU).o,$(OBJS))
 # actor experiment builds: make expt_actor EXPT='-DQCART_MCONV_Q=4' NAME=q4
 expt_actor:
 	@mkdir -p $(CSRC)/build_$(NAME)

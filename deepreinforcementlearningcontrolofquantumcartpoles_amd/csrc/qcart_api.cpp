@@ -132,7 +132,8 @@ int upload(qc_handle* h, T** dst, const T* src, size_t n) {
 int upload_tables(qc_handle* h) {
     const int Np = h->op.Npad, kl = h->op.kl, R = h->op.R;
     const bool f32 = h->p.precision == QC_FP32;   // fp32 blocks: the fp64 factors rounded once
-    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u);
+    const bool sym = !h->op.fock;   // grid: L D L^T, no uc band (SlotLayout)
+    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u, sym);
     h->slot_bytes = L.bytes;
     std::vector<uint8_t> tab((size_t)kMaxSlots * L.bytes, 0);
     std::vector<double> force(kMaxSlots, 0.0);
@@ -152,7 +153,7 @@ int upload_tables(qc_handle* h) {
         for (int b = 0; b < kl; b++)
             for (int r = 0; r < Np; r++) {
                 put(blk, L.lc, ilv(b, r), a.lc[(size_t)b * Np + r]);
-                put(blk, L.uc, ilv(b, r), a.uc[(size_t)b * Np + r]);
+                if (!sym) put(blk, L.uc, ilv(b, r), a.uc[(size_t)b * Np + r]);
             }
         for (int r = 0; r < Np; r++) put(blk, L.di, ilv(0, r), a.dinv[r]);
         if (h->op.family == QC_IHO)
@@ -223,12 +224,13 @@ KArgs base_args(const qc_handle* h) {
         }
         const bool f32 = p.precision == QC_FP32;
         const uint32_t es = f32 ? 8u : 16u;   // bytes per complex table element
-        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO, es);
-        // MODE 2 image: levels 0..3 + the row prefix per direction at fixed places (needs kf, kb <= 4)
-        const size_t t1 = L.tf, t2 = L.tf + (size_t)10 * op.kl * op.kl * kWave * es;
+        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO, es, !op.fock);
+        // MODE 2 image: levels 0..NL-1 + the row prefix per direction at fixed places (needs kf, kb <= NL)
+        const int NL = mode2_levels(op.kl);
+        const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * kWave * es;
         // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
         const size_t fx = (op.fock && !f32) ? (size_t)(op.R + 1) * kWave * 8 : 0;
-        int mode = (t2 + fx <= 160 * 1024 && lf <= 4 && lb <= 4) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
+        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
         a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);

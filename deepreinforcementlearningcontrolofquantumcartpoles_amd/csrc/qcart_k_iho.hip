@@ -19,12 +19,3 @@ int launch_fam1(int R, int kind, const KArgs& a, int what, double xth, void* out
 }
 
 }  // namespace qcart
-
-#ifdef QCART_STAMPS
-// diagnostic build: read and clear the per-phase cycle sums of the IHO step kernel
-extern "C" int qc_debug_stamps(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qcart::qc_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    unsigned long long z[16] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(qcart::qc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -9,26 +9,33 @@ namespace qcart {
 // (v*kl*kl + e)*64 + l. A wave's j-th read of a band is then one contiguous 64-element run, and the
 // step kernel addresses the block with one buffer descriptor and constant offsets.
 //   lc   complex [kl][R][64]    L[r][r-k]                      (zgbtrs forward)
-//   uc   complex [kl][R][64]    U[r][r+k] / U[r][r]            (zgbtrs backward)
+//   uc   complex [kl][R][64]    U[r][r+k] / U[r][r]            (zgbtrs backward; absent when sym)
 //   di   complex [R][64]        1 / U[r][r]
 //   m2   real    [10][R][64]    2 Im A[r-d][r] (IHO only; zero unless the reference mirror mode)
 //   tf   complex [7][kl*kl][64] forward Kogge-Stone composites, level 6 = in-row prefix product
 //   tb   complex [7][kl*kl][64] backward composites, level 6 = in-row suffix product
+// sym (grid families): ab = I + i dt/2 H_F is complex symmetric, so its pivot-free LU is L D L^T and
+// U[r][r+k] / U[r][r] = L[r+k][r]: the backward substitution reads the lc band at row r + k (the next
+// lane's run for rows past the lane) and the block carries no uc band.
 struct SlotLayout {
     uint32_t lc, uc, di, m2, tf, tb, bytes;
 };
 // es: bytes of one complex element (16 fp64, 8 fp32); real bands use es / 2
-constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16) {
+constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, bool sym = false) {
     SlotLayout L{};
     L.lc = 0;
     L.uc = L.lc + es * 64u * (uint32_t)(kl * R);
-    L.di = L.uc + es * 64u * (uint32_t)(kl * R);
+    L.di = L.uc + (sym ? 0u : es * 64u * (uint32_t)(kl * R));
     L.m2 = L.di + es * 64u * (uint32_t)R;
     L.tf = L.m2 + (has_m2 ? (es / 2) * 64u * 10u * (uint32_t)R : 0u);
     L.tb = L.tf + es * 64u * 7u * (uint32_t)(kl * kl);
     L.bytes = L.tb + es * 64u * 7u * (uint32_t)(kl * kl);
     return L;
 }
+
+// scan levels per direction the MODE 2 LDS image keeps (forward levels, prefix, backward levels, suffix):
+// 4 for the Fock bands (kl <= 2), 2 for the grid's kl = 4 (its 16-element composites)
+constexpr int mode2_levels(int kl) { return kl >= 4 ? 2 : 4; }
 
 struct KArgs {
     // state and I/O (device pointers)

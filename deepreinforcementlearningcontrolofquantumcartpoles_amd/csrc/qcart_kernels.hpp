@@ -749,17 +749,29 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
 #endif
 // Composite level offsets: forward level l at f0 + l*C, row prefix at fP; backward at b0 + l*C, bP
 // (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
-template <int KL, int R, int MODE, bool M2, typename RT>
+// SYM (grid): the backward factor U[r][r+1+k] / U[r][r] is read as L[r+1+k][r] from the lc band (row
+// r + 1 + k: the same lane's run, or a following lane's — dl elements further — past the lane's rows).
+template <int KL, int R, int MODE, bool M2, bool SYM, typename RT>
 __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& tb, int kf, int kb,
                                            int lane QC_SOLVE_STAMP_ARGS) {
     constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
-    constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>));
+    constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>), SYM);
     constexpr uint32_t CB = KL * KL * CE;
-    // MODE 2 image (fixed, compile-time offsets): forward levels 0..3, forward P, backward 0..3, backward P
-    // (the host uses MODE 2 only when every slot keeps <= 4 levels per direction)
-    constexpr uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + 4u * CB : SL.tf + 6u * CB;
-    constexpr uint32_t b0 = MODE == 2 ? SL.tf + 5u * CB : SL.tb;
-    constexpr uint32_t bP = MODE == 2 ? SL.tf + 9u * CB : SL.tb + 6u * CB;
+    // MODE 2 image (fixed, compile-time offsets): forward levels 0..NL-1, forward P, backward 0..NL-1,
+    // backward P (the host uses MODE 2 only when every slot keeps <= NL levels per direction)
+    constexpr uint32_t NL = (uint32_t)mode2_levels(KL);
+    constexpr uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + NL * CB : SL.tf + 6u * CB;
+    constexpr uint32_t b0 = MODE == 2 ? SL.tf + (NL + 1u) * CB : SL.tb;
+    constexpr uint32_t bP = MODE == 2 ? SL.tf + (2u * NL + 1u) * CB : SL.tb + 6u * CB;
+    // backward factor k of row j (k = 0..KL-1 multiplies x_{j+1+k})
+    auto ucf = [&](const Tab<MODE, RT>& t, int k, int j) -> cx<RT> {
+        if constexpr (SYM) {
+            const int r = j + 1 + k, dl = r / R;   // row r of this lane = row r - dl R of lane + dl
+            return t.c(SL.lc + (uint32_t)(k * R + r - dl * R) * CE + (uint32_t)(dl * (int)sizeof(cx<RT>)));
+        } else {
+            return t.c(SL.uc + (uint32_t)(k * R + j) * CE);
+        }
+    };
     const bool hf = MODE == 2 || kf <= 4, hb = MODE == 2 || kb <= 4;
     // forward, pass 1 (zero incoming state): lane end state e_l
     cx<RT> s[KL];
@@ -824,7 +836,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
         cx<RT> x = b[j];
 #pragma unroll
         for (int k = KL - 1; k >= 0; --k)   // s[k] = x_{j+1+k}: zero for j + k >= R - 1
-            if (j + k < R - 1) x = cmsub(x, tb.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
+            if (j + k < R - 1) x = cmsub(x, ucf(tb, k, j), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -858,7 +870,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     for (int j = R - 1; j >= 0; --j) {
         cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, tb3.c(SL.uc + (uint32_t)(k * R + j) * CE), s[k]);
+        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ucf(tb3, k, j), s[k]);
 #pragma unroll
         for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
         s[0] = x;
@@ -995,7 +1007,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     const KArgs a) {
     constexpr int KL = Fam<FAM>::KL;
     constexpr int W = kStepWaves<FAM, R, RT>;
-    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>));
+    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), FAM == 2);
     constexpr uint32_t CE = 64u * sizeof(cx<RT>), CR = 64u * sizeof(RT);   // lane-run bytes
     const int lane = threadIdx.x & 63;
     // env of this wave: a.order (envs grouped by force slot, W per block, -1 = idle) or identity
@@ -1031,11 +1043,11 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         };
         copy(0, 0, SL.tf);
         if constexpr (MODE == 2) {   // the kept composite levels at their fixed places (band_solve)
-            constexpr uint32_t CB = KL * KL * CE;
+            constexpr uint32_t CB = KL * KL * CE, NL = (uint32_t)mode2_levels(KL);
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
-            copy(SL.tf + 6u * CB, SL.tf + 4u * CB, CB);
-            copy(SL.tb, SL.tf + 5u * CB, (uint32_t)kb * CB);
-            copy(SL.tb + 6u * CB, SL.tf + 9u * CB, CB);
+            copy(SL.tf + 6u * CB, SL.tf + NL * CB, CB);
+            copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
+            copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
         }
         if constexpr (FXL) {
             if (threadIdx.x < 64) {
@@ -1234,7 +1246,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 }
             }
             QC_STAMP(7);
-            band_solve<KL, R, MODE, false>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
+            band_solve<KL, R, MODE, false, true>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
             QC_STAMP(8);
             {
                 // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
@@ -1428,7 +1440,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R, MODE, FAM == 1>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);
+        band_solve<KL, R, MODE, FAM == 1, false>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);
         QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
@@ -1850,3 +1862,13 @@ int launch_f32(int family, int R, int kind, const KArgs& a, int what, double xth
                const double* s_arr, void* stream);
 
 }  // namespace qcart
+
+#ifdef QCART_STAMPS
+// diagnostic build: read and clear the per-phase cycle sums of the step kernel of the translation unit built
+// with -DQCART_STAMPS (weak: an experiment build stamps one family TU)
+extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qcart::qc_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(qcart::qc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

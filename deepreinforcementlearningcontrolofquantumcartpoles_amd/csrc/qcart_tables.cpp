@@ -208,6 +208,13 @@ int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost
             if (r + k < N) act.uc[(size_t)(k - 1) * Np + r] = cm(Wat(r, k), di);
         }
     }
+    // grid: ab is complex symmetric (H_F real symmetric), so U[r][r+k] / U[r][r] = L[r+k][r] up to rounding;
+    // the step kernel reads the backward factors from the lc band (SlotLayout sym), so the backward
+    // composites are built from exactly those values
+    if (!op.fock)
+        for (int k = 1; k <= kl; k++)
+            for (int r = 0; r < Np; r++)
+                act.uc[(size_t)(k - 1) * Np + r] = (r + k < Np) ? act.lc[(size_t)(k - 1) * Np + r + k] : cplx(0, 0);
     // ---- Kogge-Stone composites. Forward state s_r = (y_r, ..., y_{r-kl+1}),
     // s_r = A_r s_{r-1} + b_r e1, A_r = [[-l_1 .. -l_kl], shift]. Lane transition Phi_l = A_{lR+R-1}..A_{lR}.
     auto fwd_row = [&](int r) {

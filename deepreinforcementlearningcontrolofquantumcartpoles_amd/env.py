@@ -141,7 +141,11 @@ class BatchedEnv:
         until energy < init_energy_cutoff and no Fail."""
         todo = mask.clone()
         dt = self.ph.dt
+        rounds = 0
         while bool(todo.any()):
+            rounds += 1
+            if rounds > 1000:   # the reference redraws without bound; a broken scheme would spin forever
+                raise RuntimeError("quartic cooling reset: no acceptable initial state after 1000 redraws")
             k = (torch.rand(self.B, generator=self.gen, device=self.dev, dtype=torch.float64) * 0.6 - 0.3)
             mu = torch.zeros(self.B, dtype=torch.float64, device=self.dev)
             sg = torch.ones(self.B, dtype=torch.float64, device=self.dev)

@@ -19,13 +19,22 @@ PHASES = ["noise+D1", "term7", "mirror", "Y means", "+branch", "-branch", "Phi",
 
 
 def main():
-    n_max = int(sys.argv[1]) if len(sys.argv) > 1 else 511
-    a_mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-    B = 16384
-    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max, a_mode=a_mode)
+    # argv: <n_max> [a_mode] (IHO) or a bench config name (C3, C4, ...) [batch]
+    if len(sys.argv) > 1 and sys.argv[1] in cfg.BENCH_CONFIGS:
+        conf = cfg.BENCH_CONFIGS[sys.argv[1]]
+        ph, a_mode = conf["physics"], -1
+        B = int(sys.argv[2]) if len(sys.argv) > 2 else min(conf["batch"], 16384)
+    else:
+        n_max = int(sys.argv[1]) if len(sys.argv) > 1 else 511
+        a_mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+        B = 16384
+        ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max, a_mode=a_mode)
     st = Stepper(ph, B, 0, seed=1)
     psi = st.new_state()
-    st.reset(psi, 1, arg0=16)
+    if ph.fock:
+        st.reset(psi, 1, arg0=16)
+    else:
+        st.reset(psi, 2, arg0=0.0, arg1=0.0, arg2=1.0)
     acts = torch.randint(0, 21, (B,), device="cuda", dtype=torch.int32)
     L = _lib.lib()
     f = L.qc_debug_stamps
@@ -38,7 +47,7 @@ def main():
     torch.cuda.synchronize()
     f(buf)
     tot = sum(buf)
-    print(f"IHO N={ph.dim} a_mode={a_mode}: total {tot / (B * 80):.0f} cycles per wave-step (stamped build)")
+    print(f"family {ph.family} N={ph.dim} a_mode={a_mode} B={B}: total {tot / (B * 80):.0f} cycles per wave-step (stamped build)")
     for name, v in zip(PHASES, buf):
         print(f"  {name:10s} {v / (B * 80):8.0f} cyc  {100 * v / tot:5.1f} %")
 

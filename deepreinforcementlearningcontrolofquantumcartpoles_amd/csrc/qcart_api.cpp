@@ -228,8 +228,10 @@ KArgs base_args(const qc_handle* h) {
         // MODE 2 image: levels 0..NL-1 + the row prefix per direction at fixed places (needs kf, kb <= NL)
         const int NL = mode2_levels(op.kl);
         const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * kWave * es;
-        // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane)
-        const size_t fx = (op.fock && !f32) ? (size_t)(op.R + 1) * kWave * 8 : 0;
+        // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane), the grid its
+        // row constants (H_F's folded diagonal and x_r: 2R doubles per lane, RowLds)
+        const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
+                                  : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
         int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;

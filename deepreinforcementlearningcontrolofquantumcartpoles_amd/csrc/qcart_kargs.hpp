@@ -36,6 +36,10 @@ constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, b
 // scan levels per direction the MODE 2 LDS image keeps (forward levels, prefix, backward levels, suffix):
 // 4 for the Fock bands (kl <= 2), 2 for the grid's kl = 4 (its 16-element composites)
 constexpr int mode2_levels(int kl) { return kl >= 4 ? 2 : 4; }
+// grid step kernels that read their per-row constants (H_F's folded diagonal, x_r) from the LDS image
+// instead of holding them in registers: the R = 17 kernel, whose step spills (for R <= 9 the registers
+// are there and the LDS reads cost more than they save: C4 12.6 -> 14.9 ms, C3 29.4 -> 27.9 ms)
+constexpr bool grid_rows_in_lds(int R) { return R >= 17; }
 
 struct KArgs {
     // state and I/O (device pointers)

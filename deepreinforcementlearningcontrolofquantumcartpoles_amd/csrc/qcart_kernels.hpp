@@ -468,23 +468,59 @@ __device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, 
     }
 }
 
+// padding rows (>= N) of a grid stencil output: the high word cleared (one v_cndmask instead of two per
+// fp64 value) leaves at most |lo| 2^-1074 < 2^-1042: the padding rows stay below 1e-313 through every
+// application, so what they feed back into the real rows' stencils (x hoff ~ 1e4) is ~270 orders of magnitude
+// below a real row's rounding; their squares vanish from the norm and the moments. QCART_PAD_EXACT: exact zeros.
+__device__ __forceinline__ double pad_flush(double v, bool in) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned hi = in ? (unsigned)(u >> 32) : 0u;
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | (u & 0xffffffffull)));
+}
+__device__ __forceinline__ float pad_flush(float v, bool in) { return in ? v : 0.0f; }
+
+// grid per-row constants of the step: H_F's folded diagonal hfd_r = H_rr - cF x_r and x_r. RowReg holds
+// them in registers (MODE 0); RowLds reads them from the block's LDS image (MODE >= 1: the slot's force is
+// the block's), [hfd: R][x: R] runs of 64 doubles at the lane's offset vo — a step takes a fresh opaque vo
+// per phase, so the compiler re-reads them instead of keeping 2R doubles live across the step
+template <int R>
+struct RowReg {
+    const double (&hd)[R];
+    const double (&xg)[R];
+    __device__ __forceinline__ double h(int j) const { return hd[j]; }
+    __device__ __forceinline__ double x(int j) const { return xg[j]; }
+};
+template <int R>
+struct RowLds {
+    const char* p;
+    int vo;
+    __device__ __forceinline__ double h(int j) const { return *(const double*)(p + vo + j * 512); }
+    __device__ __forceinline__ double x(int j) const { return *(const double*)(p + vo + (R + j) * 512); }
+};
+
 // grid H_F v row by row with the folded diagonal hfd_r = H_rr - cF x_r (X is diagonal on the grid):
 // f(j, (H_F v)_j.re, (H_F v)_j.im); padding rows (>= N) give 0
-template <int R, typename RT, typename F>
-__device__ __forceinline__ void grid_hf_rows(const cx<RT> (&v)[R], const RT (&hfd)[R], const Coef<2, R, RT>& cf, int lane,
+template <int R, typename RT, typename RC, typename F>
+__device__ __forceinline__ void grid_hf_rows(const cx<RT> (&v)[R], const RC& rc, const Coef<2, R, RT>& cf, int lane,
                                              F&& f) {
     cx<RT> e[R + 8];
     make_ext<R, 4>(v, e, lane);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        RT re = hfd[j] * v[j].re, im = hfd[j] * v[j].im;
+        const RT hd = (RT)rc.h(j);
+        RT re = hd * v[j].re, im = hd * v[j].im;
 #pragma unroll
         for (int d = 1; d <= 4; ++d) {
             re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
             im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
         }
+#ifdef QCART_PAD_EXACT
         const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
         f(j, in ? re : RT(0), in ? im : RT(0));
+#else
+        const bool in = (cf.base + j) < cf.N;
+        f(j, pad_flush(re, in), pad_flush(im, in));
+#endif
     }
 }
 
@@ -1049,6 +1085,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
             copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
         }
+        if constexpr (FAM == 2 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x as [j][lane]
+            for (int i = threadIdx.x; i < R * 64; i += 64 * W) {
+                const int j = i >> 6, r = (i & 63) * R + j;
+                const double x = a.xg[r];
+                *(double*)(img + a.lds_fx + i * 8) = (double)((RT)a.hu[r] - cF * (RT)x);
+                *(double*)(img + a.lds_fx + (R * 64 + i) * 8) = x;
+            }
+        }
         if constexpr (FXL) {
             if (threadIdx.x < 64) {
 #pragma unroll
@@ -1076,12 +1120,25 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)
     cx<RT> xp[FAM == 2 ? 1 : R];
     if constexpr (FAM != 2) apply_x<FAM, R>(psi, xp, cf, lane);
-    // grid: H_F's diagonal with the slot's force folded in, once per call
-    RT hfd[FAM == 2 ? R : 1];
-    if constexpr (FAM == 2) {
+    // grid: H_F's diagonal with the slot's force folded in, once per call (MODE 0: registers; MODE >= 1:
+    // the block's LDS image, RowLds)
+    constexpr bool RCL = FAM == 2 && MODE >= 1 && grid_rows_in_lds(R);
+    RT hfd[FAM == 2 && !RCL ? R : 1];
+    if constexpr (FAM == 2 && !RCL) {
 #pragma unroll
         for (int j = 0; j < R; ++j) hfd[j] = cf.hu[j] - cF * cf.xg[j];
     }
+    auto rowc = [&]() {
+        if constexpr (RCL) {
+            int vo = lane * 8;
+            asm volatile("" : "+v"(vo));
+            return RowLds<R>{(const char*)smem_dyn + a.lds_fx, vo};
+        } else if constexpr (FAM == 2) {
+            return RowReg<R>{hfd, cf.xg};
+        } else {
+            return 0;
+        }
+    };
     RT xbar;
     int term = -1, fail = 0;
     {
@@ -1158,14 +1215,18 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             // body below (go_one_step, QO/simulation_quart.cpp:569-624), term by term.
             cx<RT> acc[R], D1[R];
             auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
-                grid_hf_rows<R>(v, hfd, cf, lane, [&](int j, RT re, RT im) { u[j] = C(re, im); });
+                const auto rc = rowc();
+                grid_hf_rows<R>(v, rc, cf, lane, [&](int j, RT re, RT im) { u[j] = C(re, im); });
             };
             // A: D1 = -i H_F psi - g/4 (x - xbar)^2 psi   (D1, QO:434-459)
             hf(psi, D1);
+            {
+            const auto rc = rowc();
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const RT xr = cf.xg[j] - xbar, q = g4r * xr * xr;
+                const RT xr = (RT)rc.x(j) - xbar, q = g4r * xr * xr;
                 D1[j] = C(D1[j].im - q * psi[j].re, -D1[j].re - q * psi[j].im);
+            }
             }
             QC_STAMP(1);
             // B: term7 = A D1 by Horner in H_F on A / a5 (QO:414-425, :631)
@@ -1185,9 +1246,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 hf(t, acc);
                 hf(acc, t);
                 // acc = psi + kA rel + k2 D1 + a5 t; Y0 = psi + dt D1; Y-+ = Y0 -+ kY rel (Y+ in psi)
+                const auto rc = rowc();
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const RT xr = cf.xg[j] - xbar;
+                    const RT xr = (RT)rc.x(j) - xbar;
                     const cx<RT> rl = C(xr * psi[j].re, xr * psi[j].im);
                     acc[j] = C(psi[j].re + kA * rl.re + k2 * D1[j].re + a5r * t[j].re,
                                psi[j].im + kA * rl.im + k2 * D1[j].im + a5r * t[j].im);
@@ -1203,10 +1265,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             {
                 // unnormalised means of Y+ and Y- (x |Y|^2 summed; D1ImRe QO:461-486)
                 double sm[2] = {0.0, 0.0};
+                const auto rc = rowc();
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    sm[0] += (double)(cf.xg[j] * (psi[j].re * psi[j].re + psi[j].im * psi[j].im));
-                    sm[1] += (double)(cf.xg[j] * (Ym[j].re * Ym[j].re + Ym[j].im * Ym[j].im));
+                    const RT x = (RT)rc.x(j);
+                    sm[0] += (double)(x * (psi[j].re * psi[j].re + psi[j].im * psi[j].im));
+                    sm[1] += (double)(x * (Ym[j].re * Ym[j].re + Ym[j].im * Ym[j].im));
                 }
                 step_sum<2>(sm);
                 yp = a.w * sm[0];
@@ -1216,8 +1280,9 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 // Y- branch: acc -= (c1 - c6) (-i H_F Y-); acc += (kRe x + kDm) rel-, rel- = (x - ym) Y-
                 const double kRed = -(c2 - c1) * g4;
                 const RT kRe = (RT)kRed, kDm = (RT)((c4 - c3 + c5) * beta - kRed * ym), ymr = (RT)ym;
-                grid_hf_rows<R>(Ym, hfd, cf, lane, [&](int j, RT hre, RT him) {
-                    const RT cr = (kRe * cf.xg[j] + kDm) * (cf.xg[j] - ymr);
+                const auto rc = rowc();
+                grid_hf_rows<R>(Ym, rc, cf, lane, [&](int j, RT hre, RT him) {
+                    const RT x = (RT)rc.x(j), cr = (kRe * x + kDm) * (x - ymr);
                     acc[j] = C(acc[j].re - kIm * him + cr * Ym[j].re, acc[j].im + kIm * hre + cr * Ym[j].im);
                 });
             }
@@ -1227,11 +1292,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 // <Y+, X rel+> + <rel+, X Y+> = 2 x (x - yp) |Y+|^2 and <rel+, X rel+> = x (x - yp)^2 |Y+|^2
                 const RT ypr = (RT)yp;
                 double d2[2] = {0.0, 0.0};
-                grid_hf_rows<R>(psi, hfd, cf, lane, [&](int j, RT hre, RT him) {
+                const auto rc = rowc();
+                grid_hf_rows<R>(psi, rc, cf, lane, [&](int j, RT hre, RT him) {
                     acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);
-                    const RT xr = cf.xg[j] - ypr, p2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
-                    d2[0] += (double)(2 * cf.xg[j] * xr * p2);
-                    d2[1] += (double)(cf.xg[j] * xr * xr * p2);
+                    const RT x = (RT)rc.x(j), xr = x - ypr, p2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
+                    d2[0] += (double)(2 * x * xr * p2);
+                    d2[1] += (double)(x * xr * xr * p2);
                 });
                 step_sum<2>(d2);
                 QC_STAMP(6);
@@ -1239,9 +1305,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
                 // acc += fx X rel+ + fy Y+ + fr rel+ = (fx x (x - yp) + fy + fr (x - yp)) Y+
                 const RT fx = (RT)(kRed + 2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(kDpd - k5 * kP * spm);
+                const auto rc2 = rowc();
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    const RT xr = cf.xg[j] - ypr, cr = (fx * cf.xg[j] + fr) * xr + fy;
+                    const RT x = (RT)rc2.x(j), xr = x - ypr, cr = (fx * x + fr) * xr + fy;
                     acc[j] = C(acc[j].re + cr * psi[j].re, acc[j].im + cr * psi[j].im);
                 }
             }
@@ -1251,11 +1318,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             {
                 // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
                 double s[2] = {0.0, 0.0}, pwin = 0.0, stop = 0.0, sbot = 0.0, ptop = 0.0, pbot = 0.0;
+                const auto rc = rowc();
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
                     s[0] += p2;
-                    s[1] += (double)cf.xg[j] * p2;
+                    s[1] += rc.x(j) * p2;
                     const int r = base + j;
                     if (r >= N - a.bnd_len && r < N) ptop += p2;
                     if (r < a.bnd_len) pbot += p2;
@@ -1512,6 +1580,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     if (lane == 0)
         for (int i = 0; i < 16; ++i) atomicAdd(&qc_stamps[i], st_acc[i]);
 #endif
+    if constexpr (RCL) load_coef<FAM, R>(cf, a, base);   // x_r for grid_obs (not held across the loop)
     // write back
 #pragma unroll
     for (int j = 0; j < R; ++j)

@@ -257,6 +257,20 @@ KArgs base_args(const qc_handle* h) {
     a.a3 = dt * dt * dt * dt / 24.;
     a.a4 = dt * dt * dt * dt * dt / 80.;
     a.a5 = dt * dt * dt * dt * dt * dt / 360.;
+    // host-folded step constants (KArgs): the same expressions the kernel evaluated
+    a.inv_sdt = 1.0 / a.sqrt_dt;
+    a.inv_dt = 1.0 / dt;
+    a.k_hisdt = 0.5 * a.inv_sdt;
+    a.k_qisdt = 0.25 * a.inv_sdt;
+    a.k_hidt = 0.5 * a.inv_dt;
+    a.k_qidt = 0.25 * a.inv_dt;
+    a.k_qdt = 0.25 * dt;
+    a.k_qsdt = 0.25 * a.sqrt_dt;
+    a.k_dz = a.sqrt_dt * dt * 0.5;
+    a.k_sb = a.sqrt_dt * a.beta;
+    a.b2 = a.a2 / a.a5;
+    a.b3 = a.a3 / a.a5;
+    a.b4 = a.a4 / a.a5;
     // check_boundary_error thresholds: IHO 2e-3 (IHO:423), HO 1e-3 (HO:404), grid 5e-3 (QO:561)
     a.fail_thr = p.family == QC_HO ? 1e-3 : (p.family == QC_IHO ? 2e-3 : 5e-3);
     for (int d = 0; d < 5; d++) a.hoff[d] = op.hoff[d];

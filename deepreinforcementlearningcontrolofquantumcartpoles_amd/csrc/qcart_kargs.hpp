@@ -93,6 +93,11 @@ struct KArgs {
     int32_t ctl_strategy;      // enum qc_control_strategy
     int32_t ctl_half;          // no_action_choice (10)
     double ctl_param, ctl_time, ctl_scaling, ctl_fmax, ctl_lambda, ctl_mass;
+    // step constants folded on the host (kernel arguments live in SGPRs; computed on the device they
+    // were wave-uniform VGPR values that the step kernel spilled): 1/sqrt(dt), 1/dt, the SRK coefficient
+    // prefactors 0.5/sqrt(dt), 0.25/sqrt(dt), 0.5/dt, 0.25/dt, 0.25 dt, 0.25 sqrt(dt), sqrt(dt) dt 0.5,
+    // sqrt(dt) beta and the Horner ratios a2/a5, a3/a5, a4/a5 — each the same fp64 expression as before
+    double inv_sdt, inv_dt, k_hisdt, k_qisdt, k_hidt, k_qidt, k_qdt, k_qsdt, k_dz, k_sb, b2, b3, b4;
 };
 
 // measurement-record update (qcart_record.hip, qc_record)

@@ -1049,8 +1049,9 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     // env of this wave: a.order (envs grouped by force slot, W per block, -1 = idle) or identity
     const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * W] : (int64_t)blockIdx.x * W;
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
-    const int64_t env = a.order ? (int64_t)a.order[blockIdx.x * W + (threadIdx.x >> 6)]
-                                : (int64_t)blockIdx.x * W + (threadIdx.x >> 6);
+    // (wave-uniform: made explicit, so every env-derived address lives in SGPRs)
+    const int64_t env = (int64_t)__builtin_amdgcn_readfirstlane(
+        a.order ? a.order[blockIdx.x * W + (threadIdx.x >> 6)] : (int)(blockIdx.x * W + (threadIdx.x >> 6)));
     const bool active = env >= 0 && env < a.B;
     // force slot: per wave (MODE 0), per block (MODE >= 1: the host groups envs so that every wave of a
     // block shares its first env's slot)
@@ -1155,10 +1156,15 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
     const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
-    const double inv_sdt = 1.0 / sdt, inv_dt = 1.0 / dt;
+    // uniform step constants: host-folded kernel arguments (SGPRs) for the Fock kernels, where device-side
+    // they were VGPR values the register allocator spilled (metric: 35 spilled registers -> 0, -1.7 %); the
+    // grid kernels keep the device-side forms (their schedule measured 2-3 % faster that way). Same values.
+    constexpr bool HC = FAM != 2;
+    const double inv_sdt = HC ? a.inv_sdt : 1.0 / sdt, inv_dt = HC ? a.inv_dt : 1.0 / dt;
     // vector-facing constants at the working precision
     const RT g4r = (RT)g4, dtr = (RT)dt, a5r = (RT)a.a5;
-    const RT b2r = (RT)(a.a2 / a.a5), b3r = (RT)(a.a3 / a.a5), b4r = (RT)(a.a4 / a.a5);   // term7 Horner / a5
+    const RT b2r = (RT)(HC ? a.b2 : a.a2 / a.a5), b3r = (RT)(HC ? a.b3 : a.a3 / a.a5),
+             b4r = (RT)(HC ? a.b4 : a.a4 / a.a5);   // term7 Horner coefficients / a5
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
@@ -1191,7 +1197,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         }
         const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
         // go_one_step: IHO/simulation_i.cpp:432-489
-        const double dW = r0 * sdt, dZ = sdt * dt * 0.5 * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
+        const double dW = r0 * sdt, dZ = (HC ? a.k_dz : sdt * dt * 0.5) * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
         if (lane == 0) {
             if (a.q_out) a.q_out[(size_t)k * a.B + env] = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = (double)xbar;
@@ -1202,9 +1208,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         int lane_o = lane, hc = lane * EC + 65536, hr = lane * ER + 65536;
         asm volatile("" : "+v"(lane_o), "+v"(hc), "+v"(hr));
         const Tab<MODE, RT> tb{rs, (const char*)smem_dyn, lane_o * EC, lane_o * ER, hc, hr};
-        const double c1 = 0.5 * inv_sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 * inv_sdt * (dW * dW - dt);
-        const double c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
-        const double c6 = 0.25 * sdt * dW;
+        double c1, c2, c3, c4, c5, c6;
+        if constexpr (HC) {
+            c1 = a.k_hisdt * dZ, c2 = a.k_qdt, c3 = a.k_qisdt * (dW * dW - dt);
+            c4 = a.k_hidt * (dW * dt - dZ), c5 = a.k_qidt * (dW * dW * (1.0 / 3.0) - dt) * dW;
+            c6 = a.k_qsdt * dW;
+        } else {
+            c1 = 0.5 * inv_sdt * dZ, c2 = 0.25 * dt, c3 = 0.25 * inv_sdt * (dW * dW - dt);
+            c4 = 0.5 * inv_dt * (dW * dt - dZ), c5 = 0.25 * inv_dt * (dW * dW * (1.0 / 3.0) - dt) * dW;
+            c6 = 0.25 * sdt * dW;
+        }
 
         if constexpr (FAM == 2) {
             // Grid family (QO / IQO): X = diag(x_r), so every X product of the scheme is a per-row
@@ -1230,7 +1243,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             }
             QC_STAMP(1);
             // B: term7 = A D1 by Horner in H_F on A / a5 (QO:414-425, :631)
-            const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2), kY = (RT)(sdt * beta);
+            const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2), kY = (RT)(HC ? a.k_sb : sdt * beta);
             cx<RT> Ym[R];
             {
                 cx<RT> t[R];
@@ -1260,7 +1273,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             }
             QC_STAMP(3);
             const RT kIm = (RT)(c1 - c6);
-            const double kP = sdt * beta;
+            const double kP = HC ? a.k_sb : sdt * beta;
             double yp, ym;
             {
                 // unnormalised means of Y+ and Y- (x |Y|^2 summed; D1ImRe QO:461-486)
@@ -1428,8 +1441,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             }
         }
         QC_STAMP(3);
-        const RT kY = (RT)(sdt * beta), kIm = (RT)(c1 - c6);
-        const double kP = sdt * beta;
+        const RT kY = (RT)(HC ? a.k_sb : sdt * beta), kIm = (RT)(c1 - c6);
+        const double kP = HC ? a.k_sb : sdt * beta;
         // Y+- = Y0 +- kY rel (Y+ in psi's registers) and their unnormalised means in one reduction
         cx<RT> xYp[R];
         double yp, ym;
@@ -1581,13 +1594,18 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         for (int i = 0; i < 16; ++i) atomicAdd(&qc_stamps[i], st_acc[i]);
 #endif
     if constexpr (RCL) load_coef<FAM, R>(cf, a, base);   // x_r for grid_obs (not held across the loop)
-    // write back
+    // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
+    // across the loop)
+    {
+        int wb = lane * R;
+        asm volatile("" : "+v"(wb));
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-        if (base + j < N) {
-            gpsi[2 * (base + j)] = psi[j].re;
-            gpsi[2 * (base + j) + 1] = psi[j].im;
-        }
+        for (int j = 0; j < R; ++j)
+            if (wb + j < N) {
+                gpsi[2 * (wb + j)] = psi[j].re;
+                gpsi[2 * (wb + j) + 1] = psi[j].im;
+            }
+    }
     if (lane == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;

@@ -36,6 +36,7 @@ struct qc_handle {
     hipStream_t stream = nullptr;
     int R = 0;
     int wpb = 4;   // envs per step workgroup (step_waves)
+    int we = 1;    // waves per env of the step kernel (2: IHO at large N, rows split over a wave pair)
     bool mirror = false;
     OpHost op;
     std::vector<ActHost> acts;
@@ -130,15 +131,15 @@ int upload(qc_handle* h, T** dst, const T* src, size_t n) {
 // (re)build every slot's factor block on the host (SlotLayout, lane-interleaved) and upload them
 // (slot capacity kMaxSlots)
 int upload_tables(qc_handle* h) {
-    const int Np = h->op.Npad, kl = h->op.kl, R = h->op.R;
+    const int Np = h->op.Npad, kl = h->op.kl, R = h->op.Rs, LN = h->op.lanes;
     const bool f32 = h->p.precision == QC_FP32;   // fp32 blocks: the fp64 factors rounded once
-    const bool sym = !h->op.fock;   // grid: L D L^T, no uc band (SlotLayout)
-    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u, sym);
+    const bool sym = !h->op.fock || LN > kWave;   // L D L^T, no uc band (SlotLayout)
+    const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u, sym, LN);
     h->slot_bytes = L.bytes;
     std::vector<uint8_t> tab((size_t)kMaxSlots * L.bytes, 0);
     std::vector<double> force(kMaxSlots, 0.0);
     std::vector<int32_t> kf(kMaxSlots, 0), kb(kMaxSlots, 0);
-    auto ilv = [&](int b, int r) { return ((size_t)b * R + (r % R)) * kWave + r / R; };   // row-band element
+    auto ilv = [&](int b, int r) { return ((size_t)b * R + (r % R)) * LN + r / R; };   // row-band element
     auto putr = [&](uint8_t* blk, uint32_t off, size_t elem, double v) {
         if (f32) ((float*)(blk + off))[elem] = (float)v;
         else ((double*)(blk + off))[elem] = v;
@@ -161,9 +162,9 @@ int upload_tables(qc_handle* h) {
                 for (int r = 0; r < Np; r++) putr(blk, L.m2, ilv(b, r), a.m2[(size_t)b * Np + r]);
         const size_t kk = (size_t)kl * kl;
         for (int v = 0; v < kTabLevels; v++)
-            for (int l = 0; l < kWave; l++)
+            for (int l = 0; l < LN; l++)
                 for (size_t e = 0; e < kk; e++) {
-                    const size_t src = ((size_t)v * kWave + l) * kk + e, dst = ((size_t)v * kk + e) * kWave + l;
+                    const size_t src = ((size_t)v * LN + l) * kk + e, dst = ((size_t)v * kk + e) * LN + l;
                     put(blk, L.tf, dst, a.tf[src]);
                     put(blk, L.tb, dst, a.tb[src]);
                 }
@@ -224,21 +225,26 @@ KArgs base_args(const qc_handle* h) {
         }
         const bool f32 = p.precision == QC_FP32;
         const uint32_t es = f32 ? 8u : 16u;   // bytes per complex table element
-        const SlotLayout L = slot_layout(op.kl, op.R, op.family == QC_IHO, es, !op.fock);
+        const bool pair = h->we == 2;
+        const SlotLayout L = slot_layout(op.kl, op.Rs, op.family == QC_IHO, es, !op.fock || pair, op.lanes);
         // MODE 2 image: levels 0..NL-1 + the row prefix per direction at fixed places (needs kf, kb <= NL)
         const int NL = mode2_levels(op.kl);
-        const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * kWave * es;
+        const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * op.lanes * es;
         // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane), the grid its
         // row constants (H_F's folded diagonal and x_r: 2R doubles per lane, RowLds)
-        const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
-                                  : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
-        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
+        // (the pair kernel reads no force coefficients from LDS; its mailboxes precede the image)
+        const size_t fx = pair ? 0
+                          : op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
+                                    : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
+        const size_t mb = pair ? (size_t)8 * kPairMailbox : 0;
+        int mode = (mb + t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (mb + t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
         a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);
-        a.lds_bytes = mode ? (uint32_t)(a.lds_fx + fx) : 0;
+        a.lds_bytes = mode ? (uint32_t)(mb + a.lds_fx + fx) : (uint32_t)mb;
     }
     a.precision = p.precision;
+    a.we = h->we;
     a.order = nullptr;
     a.n_blocks = (uint32_t)((p.batch + h->wpb - 1) / h->wpb);
     a.n_obs = qc_n_obs(h);
@@ -343,7 +349,13 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
         delete h;
         return QC_ENOTBUILT;
     }
-    h->wpb = step_waves(p->family, h->R, p->precision);
+    // IHO at large N (R = 16 fp64 / 32 fp32 in one wave: one wave per SIMD, spilling): QCART_WE=2 splits
+    // each env over a wave pair at R / 2 rows per lane. Opt-in: measured slower than one wave per env
+    // (C5: 94 vs 51.6 ms per launch; DESIGN.md §4 "two waves per env")
+    const char* we_env = std::getenv("QCART_WE");
+    const bool want_pair = we_env && std::atoi(we_env) == 2 && p->family == QC_IHO && (h->R % 2 == 0) &&
+                           step_waves(p->family, h->R / 2, p->precision, 2) > 0;
+    h->wpb = want_pair ? step_waves(p->family, h->R / 2, p->precision, 2) : step_waves(p->family, h->R, p->precision);
     if (h->wpb <= 0) {
         set_create_err("no step kernel for N = " + std::to_string(probe.N));
         delete h;
@@ -351,8 +363,26 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     }
     rc = build_ops(p->family, p->n_max, p->omega, p->x_max, p->grid_size, p->lambda_, p->mass, h->R, h->op, err);
     if (rc) { set_create_err(err); delete h; return rc; }
+    if (want_pair) {
+        h->we = 2;
+        h->op.lanes = 2 * kWave;
+        h->op.Rs = h->R / 2;
+    }
     rc = build_all_actions(h);
     if (rc) { set_create_err(h->err); delete h; return rc; }
+    if (h->we == 2) {
+        // the pair kernel's scan is the two-level one (<= 4 in-row levels per direction)
+        bool ok = true;
+        for (auto& s : h->acts) ok = ok && s.kf <= 4 && s.kb <= 4;
+        if (!ok) {
+            h->we = 1;
+            h->op.lanes = kWave;
+            h->op.Rs = h->R;
+            h->wpb = step_waves(p->family, h->R, p->precision);
+            rc = build_all_actions(h);
+            if (rc) { set_create_err(h->err); delete h; return rc; }
+        }
+    }
     DeviceGuard g(device);
     const int Np = h->op.Npad;
     if ((rc = upload(h, &h->d_xu, h->op.xu.data(), Np)) || (rc = upload(h, &h->d_xg, h->op.xg.data(), Np)) ||
@@ -582,7 +612,7 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         h->ev_used += 2;
         (void)hipEventRecord(ev0, h->stream);
     }
-    int rc = launch_step(h->p.family, h->R, a, h->stream);
+    int rc = launch_step(h->p.family, h->op.Rs, a, h->stream);
     if (h->timing) (void)hipEventRecord(ev1, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
     return QC_OK;
@@ -769,6 +799,8 @@ int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, flo
                                  h->stream);
     return rc ? fail(h, QC_EHIP, "wavefunction kernel launch failed") : QC_OK;
 }
+
+int qc_step_waves_per_env(const qc_handle* h) { return h ? h->we : QC_EINVAL; }
 
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {
     if (!h || action < 0 || action >= (int)h->acts.size()) return QC_EINVAL;

@@ -45,10 +45,11 @@ bool have_kernel(int family, int R, int precision) {
     return false;
 }
 
-int step_waves(int family, int R, int precision) {
+int step_waves(int family, int R, int precision, int we) {
     KArgs a{};
     a.B = 1;
     a.precision = precision;
+    a.we = we;
     return route(family, R, 4, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr);
 }
 

@@ -21,21 +21,25 @@ struct SlotLayout {
     uint32_t lc, uc, di, m2, tf, tb, bytes;
 };
 // es: bytes of one complex element (16 fp64, 8 fp32); real bands use es / 2
-constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, bool sym = false) {
+// lanes: lanes per env (64; 128 for the two-waves-per-env step kernel) — the run length of every band
+constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, bool sym = false, int lanes = 64) {
     SlotLayout L{};
+    const uint32_t ln = (uint32_t)lanes;
     L.lc = 0;
-    L.uc = L.lc + es * 64u * (uint32_t)(kl * R);
-    L.di = L.uc + (sym ? 0u : es * 64u * (uint32_t)(kl * R));
-    L.m2 = L.di + es * 64u * (uint32_t)R;
-    L.tf = L.m2 + (has_m2 ? (es / 2) * 64u * 10u * (uint32_t)R : 0u);
-    L.tb = L.tf + es * 64u * 7u * (uint32_t)(kl * kl);
-    L.bytes = L.tb + es * 64u * 7u * (uint32_t)(kl * kl);
+    L.uc = L.lc + es * ln * (uint32_t)(kl * R);
+    L.di = L.uc + (sym ? 0u : es * ln * (uint32_t)(kl * R));
+    L.m2 = L.di + es * ln * (uint32_t)R;
+    L.tf = L.m2 + (has_m2 ? (es / 2) * ln * 10u * (uint32_t)R : 0u);
+    L.tb = L.tf + es * ln * 7u * (uint32_t)(kl * kl);
+    L.bytes = L.tb + es * ln * 7u * (uint32_t)(kl * kl);
     return L;
 }
 
 // scan levels per direction the MODE 2 LDS image keeps (forward levels, prefix, backward levels, suffix):
 // 4 for the Fock bands (kl <= 2), 2 for the grid's kl = 4 (its 16-element composites)
 constexpr int mode2_levels(int kl) { return kl >= 4 ? 2 : 4; }
+// two-waves-per-env step kernel: LDS mailbox bytes per wave (qcart_kernels.hpp kPairBytes)
+constexpr unsigned kPairMailbox = 1024;
 // grid step kernels that read their per-row constants (H_F's folded diagonal, x_r) from the LDS image
 // instead of holding them in registers: the R = 17 kernel, whose step spills (for R <= 9 the registers
 // are there and the LDS reads cost more than they save: C4 12.6 -> 14.9 ms, C3 29.4 -> 27.9 ms)
@@ -98,6 +102,7 @@ struct KArgs {
     // prefactors 0.5/sqrt(dt), 0.25/sqrt(dt), 0.5/dt, 0.25/dt, 0.25 dt, 0.25 sqrt(dt), sqrt(dt) dt 0.5,
     // sqrt(dt) beta and the Horner ratios a2/a5, a3/a5, a4/a5 — each the same fp64 expression as before
     double inv_sdt, inv_dt, k_hisdt, k_qisdt, k_hidt, k_qidt, k_qdt, k_qsdt, k_dz, k_sb, b2, b3, b4;
+    int32_t we;                // waves per env of the step kernel (1, or 2: Fock families at large N)
 };
 
 // measurement-record update (qcart_record.hip, qc_record)
@@ -139,7 +144,7 @@ int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mas
                  void* stream);
 int launch_control(int family, int R, const KArgs& a, void* stream);   // qc_control (act_out / force_out)
 bool have_kernel(int family, int R, int precision = 0);
-int step_waves(int family, int R, int precision = 0);   // envs (waves) per step-kernel workgroup
+int step_waves(int family, int R, int precision = 0, int we = 1);   // envs per step-kernel workgroup (<0: none)
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
                  int n_slots, int gran, int32_t* order, int32_t cap, void* stream);

@@ -294,6 +294,66 @@ __device__ __forceinline__ void step_sum(double (&v)[NV]) {
     wave_sum<NV>(v);
 }
 
+// ---- two waves per env (k_step WE = 2, Fock families at N > 64 R): an env's rows are split over an
+// adjacent wave pair of the workgroup, half h owning rows [64 R h, 64 R (h + 1)); the pair exchanges
+// boundary rows (stencil halos), partial sums and scan carries through a mailbox per wave at the start of
+// the dynamic LDS. Every exchange is symmetric: both waves write their part, publish the exchange's
+// sequence number and wait for the partner's — no workgroup barrier, so pairs with different step counts
+// never wait on each other. Data is double-buffered by sequence parity: a wave rewrites a buffer two
+// exchanges later, after the partner's publish of the exchange in between proved it done reading it.
+constexpr uint32_t kPairBytes = kPairMailbox;   // per wave: [0] published sequence, [16, 16 + 2 kPairData) data
+constexpr uint32_t kPairData = 448;   // two buffers, then 64 B of scratch words for non-sending lanes
+struct PLane {
+    int l;                 // lane in the wave
+    int half;              // which half of the env's rows this wave owns
+    char* me;              // this wave's mailbox
+    const char* pa;        // the partner's
+    mutable uint32_t seq;  // exchanges so far (the same count in both waves of the pair)
+    __device__ __forceinline__ operator int() const { return l; }
+};
+template <typename LT>
+inline constexpr bool kPair = false;
+template <>
+inline constexpr bool kPair<PLane> = true;
+// this wave's buffer of the next exchange
+__device__ __forceinline__ char* pl_out(const PLane& p) {
+    ++p.seq;
+    return p.me + 16 + (p.seq & 1u) * kPairData;
+}
+// publish, then wait for the partner's part of the same exchange and return its buffer
+// (no divergent branches in the exchanges: every lane stores — the same value, or to a scratch word of the
+// mailbox — and every lane loads and selects, so the step body stays one basic block between the waits)
+__device__ __forceinline__ const char* pl_swap(const PLane& p) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_store((uint32_t*)p.me, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load((const uint32_t*)p.pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < p.seq)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return p.pa + 16 + (p.seq & 1u) * kPairData;
+}
+// wave-uniform values summed over the pair (a + b == b + a: both halves get the same bits)
+template <int NV>
+__device__ __forceinline__ void pl_sum(const PLane& p, double (&v)[NV]) {
+    double* o = (double*)pl_out(p);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) o[i] = v[i];   // uniform value, every lane
+    const double* in = (const double*)pl_swap(p);
+    // (the partner's sums are wave-uniform: read into SGPRs, so everything derived stays scalar)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const unsigned long long u = (unsigned long long)__double_as_longlong(in[i]);
+        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+        v[i] = v[i] + mk_d(lo, hi);
+    }
+}
+// the step kernel's reductions over the env (one wave, or the pair)
+template <int NV, typename LT>
+__device__ __forceinline__ void step_sum(double (&v)[NV], const LT& lane) {
+    wave_sum<NV>(v);
+    if constexpr (kPair<LT>) pl_sum<NV>(lane, v);
+}
+
 // ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
 template <int FAM>
 struct Fam;
@@ -304,11 +364,51 @@ struct Fam<1> { static constexpr int KL = 2; };
 template <>
 struct Fam<2> { static constexpr int KL = 4; };
 
+// pair halos (WE = 2): half 0 sends its last H rows (the partner's lower halo), half 1 its first H rows (the
+// partner's upper halo); the lanes whose halo crosses the wave edge (half 1: rows base-H+t < 0; half 0:
+// rows base+R+t >= 64 R, zero from the in-wave DPP shifts) take them from the partner's buffer.
+// e: [H lower][R own][H upper] (UP) or [H lower] (make_lo: lower halo only).
+template <int R, int H, bool UP, typename RT, int NE>
+__device__ __forceinline__ void pl_halo(const PLane& p, const cx<RT> (&v)[R], cx<RT> (&e)[NE]) {
+    static_assert(2 * H * sizeof(RT) <= kPairData, "halo too wide for the pair mailbox");
+    RT* o = (RT*)pl_out(p);
+    RT* const sink = (RT*)(p.me + 16 + 2 * kPairData);   // scratch words of the mailbox (not read)
+    const int base = p.l * R;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int g = base + j;   // row in this half
+        const int i = p.half == 0 ? g - (64 * R - H) : g;   // mailbox row: half 0 its last H, half 1 its first H
+        const bool snd = i >= 0 && i < H && (p.half == 0 || UP);
+        RT* d = snd ? o + 2 * i : sink;
+        d[0] = v[j].re;
+        d[1] = v[j].im;
+    }
+    const RT* in = (const RT*)pl_swap(p);
+#pragma unroll
+    for (int t = 0; t < H; ++t) {
+        const int i = base + t;   // half 1, lower halo row base - H + t of half 0's last H rows
+        const bool rcv = p.half == 1 && i < H;
+        const int ic = rcv ? i : 0;
+        const cx<RT> x = C(in[2 * ic], in[2 * ic + 1]);
+        e[t] = C(rcv ? x.re : e[t].re, rcv ? x.im : e[t].im);
+    }
+    if constexpr (UP) {
+#pragma unroll
+        for (int t = 0; t < H; ++t) {
+            const int i = base + R + t - 64 * R;   // half 0, upper halo row base + R + t of half 1's first H rows
+            const bool rcv = p.half == 0 && i >= 0;
+            const int ic = rcv ? i : 0;
+            const cx<RT> x = C(in[2 * ic], in[2 * ic + 1]);
+            e[H + R + t] = C(rcv ? x.re : e[H + R + t].re, rcv ? x.im : e[H + R + t].im);
+        }
+    }
+}
+
 // ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t.
 // Lanes outside the wave read 0 (the operators have zero rows there). dl is compile-time: the shift
 // by dl lanes is dl chained DPP wave shifts.
-template <int R, int H, typename RT>
-__device__ __forceinline__ void make_ext(const cx<RT> (&v)[R], cx<RT> (&e)[R + 2 * H], int lane) {
+template <int R, int H, typename RT, typename LT>
+__device__ __forceinline__ void make_ext(const cx<RT> (&v)[R], cx<RT> (&e)[R + 2 * H], const LT& lane) {
 #pragma unroll
     for (int j = 0; j < R; ++j) e[H + j] = v[j];
 #pragma unroll
@@ -331,10 +431,11 @@ __device__ __forceinline__ void make_ext(const cx<RT> (&v)[R], cx<RT> (&e)[R + 2
         else if (dl == 3) e[H + R + t] = C(shl<3>(v[idx].re), shl<3>(v[idx].im));
         else e[H + R + t] = C(shl<4>(v[idx].re), shl<4>(v[idx].im));
     }
+    if constexpr (kPair<LT>) pl_halo<R, H, true>(lane, v, e);
 }
 // lower halo only: e[t] = row base - H + t, t < H (up to 10 rows: dl <= 10 lanes for R = 1)
-template <int R, int H, typename RT>
-__device__ __forceinline__ void make_lo(const cx<RT> (&v)[R], cx<RT> (&e)[H], int lane) {
+template <int R, int H, typename RT, typename LT>
+__device__ __forceinline__ void make_lo(const cx<RT> (&v)[R], cx<RT> (&e)[H], const LT& lane) {
 #pragma unroll
     for (int t = 0; t < H; ++t) {
         const int o = H - t;
@@ -347,10 +448,11 @@ __device__ __forceinline__ void make_lo(const cx<RT> (&v)[R], cx<RT> (&e)[H], in
             else e[t] = C(shr<4>(v[idx].re), shr<4>(v[idx].im));
         } else {
             RT re = __shfl_up(v[idx].re, dl, 64), im = __shfl_up(v[idx].im, dl, 64);
-            const bool ok = lane >= dl;
+            const bool ok = (int)lane >= dl;
             e[t] = C(ok ? re : RT(0), ok ? im : RT(0));
         }
     }
+    if constexpr (kPair<LT>) pl_halo<R, H, false>(lane, v, e);
 }
 
 // ---- per-lane operator coefficients (action independent), loaded once per call
@@ -393,8 +495,8 @@ __device__ __forceinline__ void load_coef(Coef<FAM, R, RT>& cf, const KArgs& a, 
 }
 
 // X v   (IHO/simulation_i.cpp:168-196 Fock tridiagonal; QO/simulation_quart.cpp:214-229 grid diag)
-template <int FAM, int R, typename RT>
-__device__ __forceinline__ void apply_x(const cx<RT> (&v)[R], cx<RT> (&o)[R], const Coef<FAM, R, RT>& cf, int lane) {
+template <int FAM, int R, typename RT, typename LT>
+__device__ __forceinline__ void apply_x(const cx<RT> (&v)[R], cx<RT> (&o)[R], const Coef<FAM, R, RT>& cf, const LT& lane) {
     if constexpr (FAM <= 1) {
         cx<RT> e[R + 2];
         make_ext<R, 1>(v, e, lane);
@@ -410,8 +512,8 @@ __device__ __forceinline__ void apply_x(const cx<RT> (&v)[R], cx<RT> (&o)[R], co
 
 // H v (the force-free Hamiltonian; IHO/simulation_i.cpp:75-99, HO/simulation.cpp:69-80, QO/simulation_quart.cpp:
 // 40-58)
-template <int FAM, int R, typename RT>
-__device__ __forceinline__ void apply_h(const cx<RT> (&v)[R], cx<RT> (&oh)[R], const Coef<FAM, R, RT>& cf, int lane) {
+template <int FAM, int R, typename RT, typename LT>
+__device__ __forceinline__ void apply_h(const cx<RT> (&v)[R], cx<RT> (&oh)[R], const Coef<FAM, R, RT>& cf, const LT& lane) {
     if constexpr (FAM == 0) {
 #pragma unroll
         for (int j = 0; j < R; ++j) oh[j] = C(cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
@@ -440,8 +542,8 @@ __device__ __forceinline__ void apply_h(const cx<RT> (&v)[R], cx<RT> (&oh)[R], c
 
 // H v row by row: f(j, (H v)_j.re, (H v)_j.im) for j = 0..R-1 (lets a caller consume H v without
 // materialising it)
-template <int FAM, int R, typename RT, typename F>
-__device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, RT>& cf, int lane, F&& f) {
+template <int FAM, int R, typename RT, typename LT, typename F>
+__device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, RT>& cf, const LT& lane, F&& f) {
     if constexpr (FAM == 0) {
 #pragma unroll
         for (int j = 0; j < R; ++j) f(j, cf.hu[j] * v[j].re, cf.hu[j] * v[j].im);
@@ -561,9 +663,9 @@ __device__ __forceinline__ void apply_hx(const cx<RT> (&v)[R], cx<RT> (&oh)[R], 
 }
 
 // u = H_F v = H v - cF X v
-template <int FAM, int R, typename RT>
+template <int FAM, int R, typename RT, typename LT>
 __device__ __forceinline__ void apply_hf(const cx<RT> (&v)[R], cx<RT> (&u)[R], RT cF, const Coef<FAM, R, RT>& cf,
-                                         int lane) {
+                                         const LT& lane) {
     // fused per row (no full-length H v / X v temporaries: keeps the step within 256 VGPRs)
     if constexpr (FAM == 1) {
         cx<RT> e[R + 4];
@@ -595,9 +697,9 @@ __device__ __forceinline__ void apply_hf(const cx<RT> (&v)[R], cx<RT> (&u)[R], R
 
 // u = H_F v with the force term's coefficients fx[t] = -cF X[base-1+t][base+t] (t = 0..R) read from
 // the workgroup's LDS (Fock families, tables in LDS): 8 instead of 10 FP64 ops per row
-template <int FAM, int R, typename RT, typename TabT>
+template <int FAM, int R, typename RT, typename TabT, typename LT>
 __device__ __forceinline__ void apply_hf_fx(const cx<RT> (&v)[R], cx<RT> (&u)[R], const Coef<FAM, R, RT>& cf, const TabT& tb,
-                                            uint32_t fx0, int lane) {
+                                            uint32_t fx0, const LT& lane) {
     RT fx[R + 1];
 #pragma unroll
     for (int t = 0; t <= R; ++t) fx[t] = *(const RT*)(tb.lds + tb.vr + fx0 + t * 64 * (int)sizeof(RT));
@@ -728,10 +830,10 @@ __device__ __forceinline__ cx<RT> row_shift(cx<RT> v) {
 // then one carry of the neighbouring row's end state (row_bcast:15 upward / wave_shl + row_newbcast:15
 // downward) through the in-row prefix product P. Valid when transfer products over >= 16 lanes are
 // below kScanTol (nlev <= 4); otherwise band_solve runs the full 6-level Kogge-Stone with shuffles.
-template <int KL, bool FWD, int MODE, typename RT>
+template <int KL, bool FWD, int MODE, int LE, typename RT>
 __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& tb, uint32_t lv0, uint32_t lvp,
-                                          int nlev) {
-    constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
+                                          int nlev, cx<RT> (&pre)[KL]) {
+    constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
     // composites are read level by level (KL = 4: 16 complex per level; all levels at once would
     // not fit the register file), fenced for KL = 4 so the next level's reads are not hoisted
 #pragma unroll
@@ -755,6 +857,8 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
             if constexpr (KL > 2) __builtin_amdgcn_sched_barrier(0);
         }
     }
+#pragma unroll
+    for (int k = 0; k < KL; ++k) pre[k] = s[k];   // in-row state (the pair's cross-wave carry)
     cx<RT> P[KL * KL];
 #pragma unroll
     for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * CE);
@@ -787,11 +891,11 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
 // (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
 // SYM (grid): the backward factor U[r][r+1+k] / U[r][r] is read as L[r+1+k][r] from the lc band (row
 // r + 1 + k: the same lane's run, or a following lane's — dl elements further — past the lane's rows).
-template <int KL, int R, int MODE, bool M2, bool SYM, typename RT>
+template <int KL, int R, int MODE, bool M2, bool SYM, int LE, typename RT, typename LT>
 __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& tb, int kf, int kb,
-                                           int lane QC_SOLVE_STAMP_ARGS) {
-    constexpr uint32_t CE = 64u * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
-    constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>), SYM);
+                                           const LT& lane QC_SOLVE_STAMP_ARGS) {
+    constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
+    constexpr SlotLayout SL = slot_layout(KL, R, M2, sizeof(cx<RT>), SYM, LE);
     constexpr uint32_t CB = KL * KL * CE;
     // MODE 2 image (fixed, compile-time offsets): forward levels 0..NL-1, forward P, backward 0..NL-1,
     // backward P (the host uses MODE 2 only when every slot keeps <= NL levels per direction)
@@ -808,7 +912,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
             return t.c(SL.uc + (uint32_t)(k * R + j) * CE);
         }
     };
-    const bool hf = MODE == 2 || kf <= 4, hb = MODE == 2 || kb <= 4;
+    const bool hf = MODE == 2 || kf <= 4 || kPair<LT>, hb = MODE == 2 || kb <= 4 || kPair<LT>;
+    cx<RT> pre[KL];
     // forward, pass 1 (zero incoming state): lane end state e_l
     cx<RT> s[KL];
 #pragma unroll
@@ -825,7 +930,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(10);
     if (hf) {
-        scan_rows<KL, true, MODE>(s, tb, f0, fP, kf);
+        scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf, pre);
     } else {
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
@@ -850,8 +955,39 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     Tab<MODE, RT> tb2 = tb;
     if constexpr (KL == 4) asm volatile("" : "+v"(tb2.vc), "+v"(tb2.hc));
     // incoming state from lane - 1, pass 2
+    cx<RT> fin[KL];
+    if constexpr (kPair<LT>) {
+        // half 1's first 16-lane row takes its carry from half 0's lane 63 (in-row state) through the row
+        // prefix product, and its lane 0 the pass-2 incoming state (half 0's lane 63 final state)
+        RT* o = (RT*)pl_out(lane);
+        {
+            RT* d = (lane.half == 0 && lane.l == 63) ? o : (RT*)(lane.me + 16 + 2 * kPairData);
+#pragma unroll
+            for (int k = 0; k < KL; ++k) {
+                d[4 * k] = pre[k].re, d[4 * k + 1] = pre[k].im;
+                d[4 * k + 2] = s[k].re, d[4 * k + 3] = s[k].im;
+            }
+        }
+        const RT* in = (const RT*)pl_swap(lane);
+        {
+            const bool m = lane.half == 1 && lane.l < 16;   // carry only into half 1's row 0 (a select: the
+                                                            // other lanes read the partner's stale buffer)
+#pragma unroll
+            for (int i = 0; i < KL; ++i)
+#pragma unroll
+                for (int k = 0; k < KL; ++k)
+                    s[i] = cmac(s[i], tb.comp(fP + (uint32_t)(i * KL + k) * CE), C(m ? in[4 * k] : RT(0), m ? in[4 * k + 1] : RT(0)));
+        }
+#pragma unroll
+        for (int k = 0; k < KL; ++k) fin[k] = C(in[4 * k + 2], in[4 * k + 3]);
+    }
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
+    if constexpr (kPair<LT>) {
+        const bool r = lane.half == 1 && lane.l == 0;
+#pragma unroll
+        for (int k = 0; k < KL; ++k) s[k] = C(r ? fin[k].re : s[k].re, r ? fin[k].im : s[k].im);
+    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         cx<RT> y = b[j];
@@ -879,7 +1015,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(13);
     if (hb) {
-        scan_rows<KL, false, MODE>(s, tb, b0, bP, kb);
+        scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb, pre);
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
@@ -900,8 +1036,37 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     QC_STAMP(14);
     Tab<MODE, RT> tb3 = tb;
     if constexpr (KL == 4) asm volatile("" : "+v"(tb3.vc), "+v"(tb3.hc));
+    if constexpr (kPair<LT>) {
+        // half 0's last 16-lane row takes its carry from half 1's lane 0 (in-row state) through the row
+        // suffix product, and its lane 63 the pass-2 incoming state (half 1's lane 0 final state)
+        RT* o = (RT*)pl_out(lane);
+        {
+            RT* d = (lane.half == 1 && lane.l == 0) ? o : (RT*)(lane.me + 16 + 2 * kPairData);
+#pragma unroll
+            for (int k = 0; k < KL; ++k) {
+                d[4 * k] = pre[k].re, d[4 * k + 1] = pre[k].im;
+                d[4 * k + 2] = s[k].re, d[4 * k + 3] = s[k].im;
+            }
+        }
+        const RT* in = (const RT*)pl_swap(lane);
+        {
+            const bool m = lane.half == 0 && lane.l >= 48;   // carry only into half 0's row 3
+#pragma unroll
+            for (int i = 0; i < KL; ++i)
+#pragma unroll
+                for (int k = 0; k < KL; ++k)
+                    s[i] = cmac(s[i], tb.comp(bP + (uint32_t)(i * KL + k) * CE), C(m ? in[4 * k] : RT(0), m ? in[4 * k + 1] : RT(0)));
+        }
+#pragma unroll
+        for (int k = 0; k < KL; ++k) fin[k] = C(in[4 * k + 2], in[4 * k + 3]);
+    }
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
+    if constexpr (kPair<LT>) {
+        const bool r = lane.half == 0 && lane.l == 63;
+#pragma unroll
+        for (int k = 0; k < KL; ++k) s[k] = C(r ? fin[k].re : s[k].re, r ? fin[k].im : s[k].im);
+    }
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
         cx<RT> x = b[j];
@@ -917,8 +1082,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
 // ---- observations ---------------------------------------------------------------------------
 // Fock 'xp' (IHO/main_parallel.py:129-131): [<x>, <p>, <x^2>-<x>^2, <p^2>-<p>^2, <xp+px>/2-<x><p>]
 // with the truncated operators: <x^2> = |X psi|^2, <p^2> = |P psi|^2, <xp+px>/2 = Re<X psi, P psi>.
-template <int FAM, int R, typename RT>
-__device__ __forceinline__ void fock_obs(const cx<RT> (&psi)[R], const Coef<FAM, R, RT>& cf, int lane,
+template <int FAM, int R, typename RT, typename LT>
+__device__ __forceinline__ void fock_obs(const cx<RT> (&psi)[R], const Coef<FAM, R, RT>& cf, const LT& lane,
                                          double (&o)[5]) {
     cx<RT> e[R + 2];
     make_ext<R, 1>(psi, e, lane);
@@ -935,7 +1100,7 @@ __device__ __forceinline__ void fock_obs(const cx<RT> (&psi)[R], const Coef<FAM,
         s[3] += (double)(pp.re * pp.re + pp.im * pp.im);
         s[4] += (double)(xp.re * pp.re + xp.im * pp.im);
     }
-    wave_sum<5>(s);
+    step_sum<5>(s, lane);
     o[0] = s[0];
     o[1] = s[1];
     o[2] = s[2] - s[0] * s[0];
@@ -1037,21 +1202,31 @@ template <int FAM, int R, typename RT = double>
 constexpr int kStepWaves =
     ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= QCART_W8_MAX_RG)) ? 8 : 4;
 
-template <int FAM, int R, int MODE, typename RT = double>
-__global__ __launch_bounds__((64 * kStepWaves<FAM, R, RT>))
-__attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM, R, RT> / 4)))) void k_step(
+// waves per step workgroup: WE = 2 (two waves per env) runs 4 env pairs, two waves per SIMD
+template <int FAM, int R, typename RT, int WE>
+constexpr int kBlockWaves = WE == 2 ? 8 : kStepWaves<FAM, R, RT>;
+
+template <int FAM, int R, int MODE, typename RT = double, int WE = 1>
+__global__ __launch_bounds__((64 * kBlockWaves<FAM, R, RT, WE>))
+__attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWaves<FAM, R, RT, WE> / 4)))) void k_step(
     const KArgs a) {
+    static_assert(WE == 1 || FAM == 1, "two waves per env: IHO only");
     constexpr int KL = Fam<FAM>::KL;
-    constexpr int W = kStepWaves<FAM, R, RT>;
-    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), FAM == 2);
-    constexpr uint32_t CE = 64u * sizeof(cx<RT>), CR = 64u * sizeof(RT);   // lane-run bytes
+    constexpr int W = kBlockWaves<FAM, R, RT, WE>;   // waves per block
+    constexpr int EPB = W / WE;                       // envs per block
+    constexpr int LE = 64 * WE;                       // lanes per env
+    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), FAM == 2 || WE == 2, LE);
+    constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>), CR = (uint32_t)LE * sizeof(RT);   // lane-run bytes
     const int lane = threadIdx.x & 63;
-    // env of this wave: a.order (envs grouped by force slot, W per block, -1 = idle) or identity
-    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * W] : (int64_t)blockIdx.x * W;
+    const int half = WE == 2 ? __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1u)) : 0;   // rows owned
+    const int gl = half * 64 + lane;                                   // lane of the env
+    // env of this wave: a.order (envs grouped by force slot, EPB per block, -1 = idle) or identity
+    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * EPB] : (int64_t)blockIdx.x * EPB;
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
     // (wave-uniform: made explicit, so every env-derived address lives in SGPRs)
+    const int ei = (int)(threadIdx.x >> 6) / WE;
     const int64_t env = (int64_t)__builtin_amdgcn_readfirstlane(
-        a.order ? a.order[blockIdx.x * W + (threadIdx.x >> 6)] : (int)(blockIdx.x * W + (threadIdx.x >> 6)));
+        a.order ? a.order[blockIdx.x * EPB + ei] : (int)(blockIdx.x * EPB + ei));
     const bool active = env >= 0 && env < a.B;
     // force slot: per wave (MODE 0), per block (MODE >= 1: the host groups envs so that every wave of a
     // block shares its first env's slot)
@@ -1063,16 +1238,22 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     const double cFd = a.c * a.force[slot];
     const RT cF = (RT)cFd;
     // H_F force coefficients from LDS (apply_hf_fx): fp64 Fock families with the tables in LDS
-    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8;
+    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8 && WE == 1;
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
+    // WE = 2: the pair mailboxes (kPairBytes per wave) precede the table image
+    char* const simg = (char*)smem_dyn + (WE == 2 ? W * kPairBytes : 0u);
+    if constexpr (WE == 2) {
+        if (lane == 0) *(uint32_t*)((char*)smem_dyn + (threadIdx.x >> 6) * kPairBytes) = 0u;
+    }
     // a block of the no-budget group (k_group puts envs with env_steps <= 0 in whole blocks of their
     // own) takes no step: it skips the table image
     const bool block_idle = a.order && a.env_steps && (a.env_steps[e0] <= 0 || a.n_steps <= 0);
-    if (MODE >= 1 && !block_idle) {
+    if ((MODE >= 1 && !block_idle) || WE == 2) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
         // the 4 waves for all n_steps steps
-        char* img = (char*)smem_dyn;
+        char* img = simg;
         auto copy = [&](uint32_t src, uint32_t dst, uint32_t bytes) {
+            if (MODE == 0 || block_idle) return;
             for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 64u * W * 16u) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, (int)src, 0);
                 *(uint4*)(img + dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
@@ -1086,7 +1267,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
             copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
         }
-        if constexpr (FAM == 2 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x as [j][lane]
+        if constexpr (FAM == 2 && MODE >= 1 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x
             for (int i = threadIdx.x; i < R * 64; i += 64 * W) {
                 const int j = i >> 6, r = (i & 63) * R + j;
                 const double x = a.xg[r];
@@ -1107,7 +1288,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         __syncthreads();
     }
     if (!active) return;
-    const int base = lane * R;
+    const int base = gl * R;
+    // the lane argument of the stencil / reduction / solve helpers: the lane, or the pair context
+    const auto lnv = [&]() {
+        if constexpr (WE == 2) {
+            char* mb = (char*)smem_dyn + (threadIdx.x >> 6) * kPairBytes;
+            return PLane{lane, half, mb, half ? mb - kPairBytes : mb + kPairBytes, 0u};
+        } else {
+            return lane;
+        }
+    }();
     const int N = a.N;
     Coef<FAM, R, RT> cf;
     load_coef<FAM, R>(cf, a, base);
@@ -1120,7 +1310,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     const bool win_on = a.win_hi > a.win_lo;
     // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)
     cx<RT> xp[FAM == 2 ? 1 : R];
-    if constexpr (FAM != 2) apply_x<FAM, R>(psi, xp, cf, lane);
+    if constexpr (FAM != 2) apply_x<FAM, R>(psi, xp, cf, lnv);
     // grid: H_F's diagonal with the slot's force folded in, once per call (MODE 0: registers; MODE >= 1:
     // the block's LDS image, RowLds)
     constexpr bool RCL = FAM == 2 && MODE >= 1 && grid_rows_in_lds(R);
@@ -1133,7 +1323,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         if constexpr (RCL) {
             int vo = lane * 8;
             asm volatile("" : "+v"(vo));
-            return RowLds<R>{(const char*)smem_dyn + a.lds_fx, vo};
+            return RowLds<R>{(const char*)simg + a.lds_fx, vo};
         } else if constexpr (FAM == 2) {
             return RowReg<R>{hfd, cf.xg};
         } else {
@@ -1151,7 +1341,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             const int r = base + j;
             if (r >= a.win_lo && r < a.win_hi) s[1] += (double)(psi[j].re * psi[j].re + psi[j].im * psi[j].im);
         }
-        step_sum<2>(s);
+        step_sum<2>(s, lnv);
         xbar = (RT)(a.w * s[0]);                                  // x_expct (IHO:197-203, QO:230-236)
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
@@ -1198,16 +1388,16 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = (HC ? a.k_dz : sdt * dt * 0.5) * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
-        if (lane == 0) {
+        if (lane == 0 && half == 0) {
             if (a.q_out) a.q_out[(size_t)k * a.B + env] = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = (double)xbar;
         }
         // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
         // reads and their addresses inside the step (LICM would otherwise pin them in registers)
         constexpr int EC = (int)sizeof(cx<RT>), ER = (int)sizeof(RT);
-        int lane_o = lane, hc = lane * EC + 65536, hr = lane * ER + 65536;
+        int lane_o = gl, hc = gl * EC + 65536, hr = gl * ER + 65536;
         asm volatile("" : "+v"(lane_o), "+v"(hc), "+v"(hr));
-        const Tab<MODE, RT> tb{rs, (const char*)smem_dyn, lane_o * EC, lane_o * ER, hc, hr};
+        const Tab<MODE, RT> tb{rs, (const char*)simg, lane_o * EC, lane_o * ER, hc, hr};
         double c1, c2, c3, c4, c5, c6;
         if constexpr (HC) {
             c1 = a.k_hisdt * dZ, c2 = a.k_qdt, c3 = a.k_qisdt * (dW * dW - dt);
@@ -1326,7 +1516,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 }
             }
             QC_STAMP(7);
-            band_solve<KL, R, MODE, false, true>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
+            band_solve<KL, R, MODE, false, true, 64>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
             QC_STAMP(8);
             {
                 // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
@@ -1372,14 +1562,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         cx<RT> acc[R], rel[R], D1[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
-        apply_h<FAM, R>(psi, D1, cf, lane);
+        apply_h<FAM, R>(psi, D1, cf, lnv);
 #pragma unroll
         for (int j = 0; j < R; ++j)   // D1 = -i (H psi - cF X psi)
             D1[j] = C(D1[j].im - cF * xp[j].im, -(D1[j].re - cF * xp[j].re));
         {
             cx<RT> xr[R];
             const RT gx = g4r * xbar;
-            apply_x<FAM, R>(rel, xr, cf, lane);
+            apply_x<FAM, R>(rel, xr, cf, lnv);
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 D1[j] = C(D1[j].re - g4r * xr[j].re + gx * rel[j].re, D1[j].im - g4r * xr[j].im + gx * rel[j].im);
@@ -1389,8 +1579,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3), Horner in H_F on A/a5
             // (coefficients a_k/a5; a5 applied once in the sum below: no separate i a5 D1 pass)
             auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
-                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lane);
-                else apply_hf<FAM, R>(v, u, cF, cf, lane);
+                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lnv);
+                else apply_hf<FAM, R>(v, u, cF, cf, lnv);
             };
             cx<RT> t[R];
             hf(D1, acc);
@@ -1419,7 +1609,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             if (a.mirror) {
                 constexpr int MB = 1;
                 cx<RT> lo[10];
-                make_lo<R, 10>(D1, lo, lane);
+                make_lo<R, 10>(D1, lo, lnv);
 #pragma unroll
                 for (int h = 0; h < 10 / MB; ++h) {
                     RT mv[MB][R];
@@ -1453,8 +1643,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 Ym[j] = C(psi[j].re - kY * rel[j].re, psi[j].im - kY * rel[j].im);
                 psi[j] = C(psi[j].re + kY * rel[j].re, psi[j].im + kY * rel[j].im);   // Y+
             }
-            apply_x<FAM, R>(Ym, xYm, cf, lane);
-            apply_x<FAM, R>(psi, xYp, cf, lane);
+            apply_x<FAM, R>(Ym, xYm, cf, lnv);
+            apply_x<FAM, R>(psi, xYp, cf, lnv);
             RowDot<RT> q0, q1;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -1462,20 +1652,20 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 q1.add(j == 0, Ym[j], xYm[j]);
             }
             double sm[2] = {q0.sum(), q1.sum()};
-            step_sum<2>(sm);
+            step_sum<2>(sm, lnv);
             yp = a.w * sm[0];
             ym = a.w * sm[1];
             const RT ymr = (RT)ym;
             // Y- branch: acc -= (c1-c6) (-i H_F Y-), fused row by row with H Y- (no H Y- vector)
             {
-                h_rows<FAM, R>(Ym, cf, lane, [&](int j, RT hre, RT him) {
+                h_rows<FAM, R>(Ym, cf, lnv, [&](int j, RT hre, RT him) {
                     hre -= cF * xYm[j].re;
                     him -= cF * xYm[j].im;
                     acc[j] = C(acc[j].re - kIm * him, acc[j].im + kIm * hre);
                     xYm[j] = C(xYm[j].re - ymr * Ym[j].re, xYm[j].im - ymr * Ym[j].im);   // rel-
                 });
             }
-            apply_x<FAM, R>(xYm, Ym, cf, lane);   // X rel- (Y- no longer needed)
+            apply_x<FAM, R>(xYm, Ym, cf, lnv);   // X rel- (Y- no longer needed)
             // acc += kRe (X rel- - ym rel-) + kD rel-  =  kRe X rel- + (kD - kRe ym) rel-
             const double kRed = -(c2 - c1) * g4;
             const RT kRe = (RT)kRed, kDm = (RT)((c4 - c3 + c5) * beta - kRed * ym);
@@ -1488,13 +1678,13 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
             // Y+ branch (Y+ in psi); keeps X Y+, rel+ and X rel+ for the Phi means
             cx<RT> rp[R], xrp[R];
             const RT ypr = (RT)yp;
-            h_rows<FAM, R>(psi, cf, lane, [&](int j, RT hre, RT him) {
+            h_rows<FAM, R>(psi, cf, lnv, [&](int j, RT hre, RT him) {
                 hre -= cF * xYp[j].re;
                 him -= cF * xYp[j].im;
                 acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);   // +(c1-c6) (-i H_F Y+)
                 rp[j] = C(xYp[j].re - ypr * psi[j].re, xYp[j].im - ypr * psi[j].im);   // rel+
             });
-            apply_x<FAM, R>(rp, xrp, cf, lane);
+            apply_x<FAM, R>(rp, xrp, cf, lnv);
             const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp;
             QC_STAMP(5);
             // Phi+- = Y+ +- kP rel+; X Phi+- = X Y+ +- kP X rel+, so their unnormalised means are
@@ -1507,7 +1697,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 q1.add(j == 0, rp[j], xrp[j]);
             }
             double d2[2] = {q0.sum(), q1.sum()};
-            step_sum<2>(d2);
+            step_sum<2>(d2, lnv);
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
@@ -1521,12 +1711,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R, MODE, FAM == 1, false>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);
+        band_solve<KL, R, MODE, FAM == 1, WE == 2, LE>(acc, tb, kf, kb, lnv QC_SOLVE_STAMP_PASS);
         QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
             cx<RT> xn[R];
-            apply_x<FAM, R>(acc, xn, cf, lane);
+            apply_x<FAM, R>(acc, xn, cf, lnv);
             // full reductions only for the norm and the next <x>; the boundary sums (Fail) touch the
             // few lanes holding the edge rows and are read from them directly
             double s[2] = {0.0, 0.0}, pwin = 0.0, stop = 0.0, sbot = 0.0;
@@ -1544,8 +1734,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                     if (j == jt) suf = s[0];
                 }
                 s[1] = qx.sum();
-                stop = readlane_d(suf, lt);
-                for (int l = lt + 1; l <= (N - 1) / R; ++l) stop += readlane_d(s[0], l);
+                // (lanes of the env: this wave holds env lanes [64 half, 64 half + 63])
+                const int l0 = 64 * half, l1 = (N - 1) / R;
+                if (lt >= l0 && lt < l0 + 64) stop = readlane_d(suf, lt - l0);
+                for (int l = (lt + 1 > l0 ? lt + 1 : l0); l <= l1 && l < l0 + 64; ++l) stop += readlane_d(s[0], l - l0);
             } else {
                 double ptop = 0.0, pbot = 0.0;
 #pragma unroll
@@ -1561,7 +1753,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
                 for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
             }
-            step_sum<2>(s);
+            if constexpr (WE == 2) {   // the pair's norm, next <x> and boundary sum in one exchange
+                wave_sum<2>(s);
+                double u[3] = {s[0], s[1], stop};
+                pl_sum<3>(lnv, u);
+                s[0] = u[0], s[1] = u[1], stop = u[2];
+            } else {
+                step_sum<2>(s);
+            }
             // 1/sqrt(s0): hardware estimate + two Newton steps (full fp64 precision)
             double scale = __builtin_amdgcn_rsq(s[0]);
             scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
@@ -1597,7 +1796,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
     // across the loop)
     {
-        int wb = lane * R;
+        int wb = gl * R;
         asm volatile("" : "+v"(wb));
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -1606,7 +1805,7 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
                 gpsi[2 * (wb + j) + 1] = psi[j].im;
             }
     }
-    if (lane == 0) {
+    if (lane == 0 && half == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;
         a.ctr[env] = ctr0 + (uint64_t)n_my;
@@ -1614,8 +1813,8 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     if (a.obs_out) {
         if constexpr (FAM <= 1) {
             double o[5];
-            fock_obs<FAM, R>(psi, cf, lane, o);
-            if (lane < 5) {
+            fock_obs<FAM, R>(psi, cf, lnv, o);
+            if (lane < 5 && half == 0) {
                 double v = o[0];
 #pragma unroll
                 for (int i = 1; i < 5; ++i) v = (lane == i) ? o[i] : v;
@@ -1896,21 +2095,26 @@ namespace qcart {
 
 static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
-template <int FAM, int R, int MODE, typename RT>
+template <int FAM, int R, int MODE, typename RT, int WE = 1>
 int launch_step_mode(const KArgs& a, hipStream_t st) {
-    const dim3 grid(a.n_blocks), block(64 * kStepWaves<FAM, R, RT>);
-    if (MODE >= 1) {
+    const dim3 grid(a.n_blocks), block(64 * kBlockWaves<FAM, R, RT, WE>);
+    constexpr bool lds = MODE >= 1 || WE == 2;
+    if (lds) {
         static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
         if (!attr_set) {
-            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE, RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE, RT, WE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024) != hipSuccess)
                 return -3;
             attr_set = true;
         }
     }
-    hipLaunchKernelGGL((k_step<FAM, R, MODE, RT>), grid, block, MODE >= 1 ? a.lds_bytes : 0, st, a);
+    hipLaunchKernelGGL((k_step<FAM, R, MODE, RT, WE>), grid, block, lds ? a.lds_bytes : 0, st, a);
     return 0;
 }
+// (FAM, R, RT) with a two-waves-per-env step kernel: IHO at 2 x 64 lanes x R rows, R = 8 fp64 (N <= 1024)
+// and R = 16 fp32 (N <= 2048, config C5) — each the largest R that runs two waves per SIMD
+template <int FAM, int R, typename RT>
+constexpr bool kHasPair = FAM == 1 && ((R == 8 && sizeof(RT) == 8) || (R == 16 && sizeof(RT) == 4));
 
 // per-family launch entry points, instantiated in qcart_k_{ho,iho,grid,f32}.hip
 template <int FAM, int R, typename RT = double>
@@ -1919,7 +2123,21 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
                void* stream) {
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 4) return kStepWaves<FAM, R, RT>;   // query: envs per step workgroup
+    if (kind == 4) {   // query: envs per step workgroup
+        if constexpr (kHasPair<FAM, R, RT>)
+            if (a.we == 2) return kBlockWaves<FAM, R, RT, 2> / 2;
+        return a.we == 2 ? -6 : kStepWaves<FAM, R, RT>;
+    }
+    if (kind == 0 && a.we == 2) {
+        if constexpr (kHasPair<FAM, R, RT>) {
+            const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, 2>(a, st)
+                         : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT, 2>(a, st)
+                                           : launch_step_mode<FAM, R, 0, RT, 2>(a, st);
+            if (rc) return rc;
+            return hipGetLastError() == hipSuccess ? 0 : -3;
+        }
+        return -6;
+    }
     if (kind == 0) {
         const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT>(a, st)
                      : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT>(a, st)

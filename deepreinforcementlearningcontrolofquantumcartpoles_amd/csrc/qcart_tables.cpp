@@ -96,6 +96,8 @@ int build_ops(int family, int n_max, double omega, double x_max, double grid_siz
     const int N = op.N, kl = op.kl;
     op.R = R;
     op.Npad = kWave * R;
+    op.lanes = kWave;
+    op.Rs = R;
     if (op.Npad < N) { err = "rows-per-lane too small"; return QC_EINVAL; }
     const int Np = op.Npad;
     op.hband.assign((size_t)(2 * kl + 1) * N, 0.0);
@@ -154,7 +156,7 @@ int build_ops(int family, int n_max, double omega, double x_max, double grid_siz
 
 // reset_ab(): IHO/simulation_i.cpp:227-277, HO/simulation.cpp:208-258, QO/simulation_quart.cpp:394-432
 int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost& act, std::string& err) {
-    const int N = op.N, kl = op.kl, Np = op.Npad, R = op.R;
+    const int N = op.N, kl = op.kl, Np = op.Npad;
     act = ActHost();
     act.force = force;
     // ---- ab = I + i dt/2 H_F, dense band W[i][d], d in [-kl, kl]
@@ -208,13 +210,15 @@ int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost
             if (r + k < N) act.uc[(size_t)(k - 1) * Np + r] = cm(Wat(r, k), di);
         }
     }
-    // grid: ab is complex symmetric (H_F real symmetric), so U[r][r+k] / U[r][r] = L[r+k][r] up to rounding;
+    // grid (and the two-waves-per-env Fock tables): ab is complex symmetric (H_F real symmetric), so
+    // U[r][r+k] / U[r][r] = L[r+k][r] up to rounding;
     // the step kernel reads the backward factors from the lc band (SlotLayout sym), so the backward
     // composites are built from exactly those values
-    if (!op.fock)
+    if (!op.fock || op.lanes > kWave)
         for (int k = 1; k <= kl; k++)
             for (int r = 0; r < Np; r++)
                 act.uc[(size_t)(k - 1) * Np + r] = (r + k < Np) ? act.lc[(size_t)(k - 1) * Np + r + k] : cplx(0, 0);
+    const int LN = op.lanes, RS = op.Rs;   // step-kernel lanes per env, rows per lane
     // ---- Kogge-Stone composites. Forward state s_r = (y_r, ..., y_{r-kl+1}),
     // s_r = A_r s_{r-1} + b_r e1, A_r = [[-l_1 .. -l_kl], shift]. Lane transition Phi_l = A_{lR+R-1}..A_{lR}.
     auto fwd_row = [&](int r) {
@@ -229,45 +233,45 @@ int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost
         for (int i = 1; i < kl; i++) B[i * kl + (i - 1)] = 1.0;
         return B;
     };
-    std::vector<Mat> Tk(kWave), Qk(kWave);
-    for (int l = 0; l < kWave; l++) {
+    std::vector<Mat> Tk(LN), Qk(LN);
+    for (int l = 0; l < LN; l++) {
         Mat P = eye(kl);
-        for (int j = 0; j < R; j++) P = matmul(fwd_row(l * R + j), P, kl);
+        for (int j = 0; j < RS; j++) P = matmul(fwd_row(l * RS + j), P, kl);
         Tk[l] = P;
         Mat Q = eye(kl);
-        for (int j = R - 1; j >= 0; j--) Q = matmul(bwd_row(l * R + j), Q, kl);
+        for (int j = RS - 1; j >= 0; j--) Q = matmul(bwd_row(l * RS + j), Q, kl);
         Qk[l] = Q;
     }
     const size_t blk = (size_t)kl * kl;
-    act.tf.assign((size_t)kTabLevels * kWave * blk, cplx(0, 0));
-    act.tb.assign((size_t)kTabLevels * kWave * blk, cplx(0, 0));
+    act.tf.assign((size_t)kTabLevels * LN * blk, cplx(0, 0));
+    act.tb.assign((size_t)kTabLevels * LN * blk, cplx(0, 0));
     // in-row (16-lane DPP row) products for the two-level scan: forward Pf(l) = Phi_l .. Phi_{row start},
     // backward Pb(l) = Psi_l .. Psi_{row end}; they carry a neighbouring row's end state into the row
     {
-        std::vector<Mat> Pf(kWave), Pb(kWave);
-        for (int l = 0; l < kWave; l++) Pf[l] = (l % 16 == 0) ? Tk[l] : matmul(Tk[l], Pf[l - 1], kl);
-        for (int l = kWave - 1; l >= 0; l--) Pb[l] = (l % 16 == 15) ? Qk[l] : matmul(Qk[l], Pb[l + 1], kl);
-        for (int l = 0; l < kWave; l++) {
-            std::copy(Pf[l].begin(), Pf[l].end(), act.tf.begin() + ((size_t)kRowPrefix * kWave + l) * blk);
-            std::copy(Pb[l].begin(), Pb[l].end(), act.tb.begin() + ((size_t)kRowPrefix * kWave + l) * blk);
+        std::vector<Mat> Pf(LN), Pb(LN);
+        for (int l = 0; l < LN; l++) Pf[l] = (l % 16 == 0) ? Tk[l] : matmul(Tk[l], Pf[l - 1], kl);
+        for (int l = LN - 1; l >= 0; l--) Pb[l] = (l % 16 == 15) ? Qk[l] : matmul(Qk[l], Pb[l + 1], kl);
+        for (int l = 0; l < LN; l++) {
+            std::copy(Pf[l].begin(), Pf[l].end(), act.tf.begin() + ((size_t)kRowPrefix * LN + l) * blk);
+            std::copy(Pb[l].begin(), Pb[l].end(), act.tb.begin() + ((size_t)kRowPrefix * LN + l) * blk);
         }
     }
     for (int lvl = 0; lvl < kMaxLevels; lvl++) {
         const int d = 1 << lvl;
         double mf = 0, mb = 0;
-        for (int l = 0; l < kWave; l++) {
+        for (int l = 0; l < LN; l++) {
             if (l >= d) mf = std::max(mf, maxabs(Tk[l]));
-            if (l + d < kWave) mb = std::max(mb, maxabs(Qk[l]));
-            std::copy(Tk[l].begin(), Tk[l].end(), act.tf.begin() + ((size_t)lvl * kWave + l) * blk);
-            std::copy(Qk[l].begin(), Qk[l].end(), act.tb.begin() + ((size_t)lvl * kWave + l) * blk);
+            if (l + d < LN) mb = std::max(mb, maxabs(Qk[l]));
+            std::copy(Tk[l].begin(), Tk[l].end(), act.tf.begin() + ((size_t)lvl * LN + l) * blk);
+            std::copy(Qk[l].begin(), Qk[l].end(), act.tb.begin() + ((size_t)lvl * LN + l) * blk);
         }
         act.max_tf[lvl] = mf;
         act.max_tb[lvl] = mb;
         // next level: T_{k+1}(l) = T_k(l) T_k(l - d);  Q_{k+1}(l) = Q_k(l) Q_k(l + d)
-        std::vector<Mat> T2(kWave), Q2(kWave);
-        for (int l = 0; l < kWave; l++) {
+        std::vector<Mat> T2(LN), Q2(LN);
+        for (int l = 0; l < LN; l++) {
             T2[l] = (l - d >= 0) ? matmul(Tk[l], Tk[l - d], kl) : Tk[l];
-            Q2[l] = (l + d < kWave) ? matmul(Qk[l], Qk[l + d], kl) : Qk[l];
+            Q2[l] = (l + d < LN) ? matmul(Qk[l], Qk[l + d], kl) : Qk[l];
         }
         Tk.swap(T2);
         Qk.swap(Q2);

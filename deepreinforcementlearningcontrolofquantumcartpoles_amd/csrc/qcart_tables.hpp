@@ -33,6 +33,9 @@ struct OpHost {
     int family = 0;      // 0 HO, 1 IHO, 2 QO, 3 IQO
     bool fock = true;
     int N = 0, kl = 0, R = 0, Npad = 0, x0 = 0;
+    // step-kernel factor tables: lanes per env and rows per lane (64 x R; 128 x R/2 for the two-waves-
+    // per-env step kernel, the same Npad)
+    int lanes = 64, Rs = 0;
     double w = 1.0;      // dot weight (1 or h)
     double c = 0.0;      // force coupling (omega or pi)
     double h = 0.0;

@@ -252,6 +252,12 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
  * action a (forward, backward), and the truncation bound used. */
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);
 
+/* Waves per env of the handle's step kernel: 1, or 2 when the handle was created with QCART_WE=2 in the
+ * environment for an IHO size whose one-wave kernel runs one wave per SIMD (N > 512 fp64, N > 1024 fp32):
+ * each env's rows are then split over a wave pair that exchanges halos, sums and scan carries through LDS
+ * (opt-in: measured slower). */
+int qc_step_waves_per_env(const qc_handle* h);
+
 /* ---------------------------------------------------------------------------------------------
  * Batched DQN actor: the reference's direct_DQN action selection
  * (inverted harmonic oscillator/RL.py:80-111 + layers.py FactorizedNoisy / Linear_weight_normalize),

@@ -56,6 +56,8 @@ CASES = {
     "iho64_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=63, gamma=0.5 * pi),
     "iho512_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=511, gamma=0.5 * pi),
     "iho512_exact_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=511, gamma=0.5 * pi, a_mode=1),
+    # N = 1024: the two-waves-per-env step kernel (R = 8 rows on each of 2 x 64 lanes)
+    "iho1024_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=1023, gamma=0.5 * pi),
     "ho256": cfg.DEFAULTS[cfg.HO].with_(n_max=255),
     "ho71": cfg.DEFAULTS[cfg.HO],
     "qo171": cfg.DEFAULTS[cfg.QO],
@@ -130,7 +132,7 @@ def run_pair(oracle_mod, ph, steps, B, act_lo, act_hi, chunk=80, seed=7, policy=
     ("iho64", 1000, 8, "pd"), ("iho181", 1000, 8, "random"), ("iho512_g05", 1000, 8, "pd"),
     ("iho512_dt2", 1000, 8, "pd"), ("iho512_exact_g05", 1000, 4, "pd"),
     ("ho256", 1000, 6, "random"), ("ho71", 1000, 8, "random"), ("qo171", 1000, 6, "random"),
-    ("iqo513", 1000, 4, "random"), ("qo1025", 1000, 3, "random"),
+    ("iqo513", 1000, 4, "random"), ("qo1025", 1000, 3, "random"), ("iho1024_g05", 1000, 4, "pd"),
 ])
 def test_psi_parity_injected_noise(oracle_mod, name, steps, B, policy):
     """||psi_GPU - psi_ref||_2 < 1e-9 after 1000 steps (fp64) for every env whose trajectory stays
@@ -395,7 +397,7 @@ def test_config_size_batch_properties(oracle_mod, config):
         assert err < 1e-10, (e, err)
 
 
-@pytest.mark.parametrize("n_max", [511, 2047])
+@pytest.mark.parametrize("n_max", [511, 1023, 2047])
 def test_fp32_path_tracks_fp64_oracle(oracle_mod, n_max):
     """fp32 working precision (config C5: IHO N = 2048 in fp32): the complex64 state stays within
     fp32 accumulation error of the fp64 oracle on identical injected noise (measured ~8e-7 at 200
@@ -446,6 +448,35 @@ def test_fp32_c5_batch_properties(oracle_mod):
                        n_threads=1)
         err = np.linalg.norm(psi[e].cpu().numpy().astype(np.complex128) - ref[0])
         assert err < 1e-5, (e, err)
+
+
+def test_pair_kernel_tracks_oracle_and_one_wave(oracle_mod, monkeypatch):
+    """The opt-in two-waves-per-env step kernel (QCART_WE=2; C5 size: IHO N = 2048 fp32, 2 x 64 lanes x 16
+    rows, halos / sums / scan carries exchanged through LDS) from random low-level Fock states, random force
+    slots and the in-kernel Philox stream: every sampled env within fp32 accuracy of the fp64 oracle, and
+    of the one-wave kernel."""
+    ph = cfg.BENCH_CONFIGS["C5"]["physics"]
+    B, steps = 64, 80
+    out = {}
+    for we in ("1", "2"):
+        monkeypatch.setenv("QCART_WE", we)
+        st = Stepper(ph, B, 0, seed=7)
+        assert st.waves_per_env == int(we)
+        psi = st.new_state()
+        st.reset(psi, 1, arg0=16)
+        psi0 = psi.clone()
+        acts = torch.randint(0, 21, (B,), generator=torch.Generator(device="cuda").manual_seed(2), device="cuda",
+                             dtype=torch.int32)
+        res = st.step(psi, acts, steps)
+        out[we] = (psi.cpu().numpy().astype(np.complex128), res["fail_step"].cpu().numpy())
+    np.testing.assert_array_equal(out["1"][1], out["2"][1])
+    assert float(np.abs(out["1"][0] - out["2"][0]).max()) < 1e-5
+    osys = oracle_sys(oracle_mod, ph)
+    for e in (0, 17, B - 1):
+        ref = psi0[e:e + 1].cpu().numpy().astype(np.complex128)
+        osys.run_batch(ref, acts[e:e + 1].cpu().numpy(), ph.f_max, steps, ph.dt, ph.gamma, seed=7, env_offset=e,
+                       n_threads=1)
+        assert np.linalg.norm(out["2"][0][e] - ref[0]) < 1e-5, e
 
 
 def test_fp32_rejects_grid_and_wrong_dtype():

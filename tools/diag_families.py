@@ -17,11 +17,17 @@ CASES = [
     ("QO N=1024 (C3)", cfg.BENCH_CONFIGS["C3"]["physics"], 16384),
     ("IQO N=513 (C4)", cfg.BENCH_CONFIGS["C4"]["physics"], 65536),
     ("IHO N=2048 fp32 (C5)", cfg.BENCH_CONFIGS["C5"]["physics"], 32768),
+    ("IHO N=1024 fp32", cfg.BENCH_CONFIGS["C5"]["physics"].with_(n_max=1023), 65536),
+    ("IHO N=512 fp32", cfg.BENCH_CONFIGS["C5"]["physics"].with_(n_max=511), 65536),
+    ("IHO N=1024 fp64", cfg.DEFAULTS[cfg.IHO].with_(n_max=1023), 32768),
 ]
 
 
 def main():
+    sel = sys.argv[1:]   # optional substrings selecting cases
     for name, ph, B in CASES:
+        if sel and not any(t in name for t in sel):
+            continue
         st = Stepper(ph, B, 0, seed=1)
         psi = st.new_state()
         if ph.fock:

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Diagnostic: the step kernel (one wave per env, QCART_WE=1, or the wave pair) against the fp64 oracle on the
+same Philox stream from a random low-level Fock state: per-env error and the rows where it sits.
+    python tools/diag_pair.py <n_max> <precision> <B> <action|-1> <steps>"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
+from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+n_max, prec, B, act, steps = (int(x) for x in sys.argv[1:6])
+ph = cfg.BENCH_CONFIGS["C5"]["physics"].with_(n_max=n_max, precision=prec)
+osys = O.OracleSystem(ph.family, n_max=ph.n_max, omega=ph.omega, x_max=ph.x_max, grid_size=ph.grid_size,
+                      lambda_=ph.lambda_, mass=ph.mass, moment_order=ph.moment_order, a_mode=ph.a_mode)
+for we in ("1", "2"):
+    os.environ["QCART_WE"] = we
+    st = Stepper(ph, B, 0, seed=7)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=16)
+    psi0 = psi.clone()
+    acts = torch.full((B,), act, dtype=torch.int32, device="cuda") if act >= 0 else torch.randint(
+        0, 21, (B,), generator=torch.Generator(device="cuda").manual_seed(2), device="cuda", dtype=torch.int32)
+    st.step(psi, acts, steps)
+    torch.cuda.synchronize()
+    e = 0
+    ref = psi0[e:e + 1].cpu().numpy().astype(np.complex128)
+    osys.run_batch(ref, acts[e:e + 1].cpu().numpy(), ph.f_max, steps, ph.dt, ph.gamma, seed=7, env_offset=e, n_threads=1)
+    got = psi[e].cpu().numpy().astype(np.complex128)
+    r = np.abs(got - ref[0])
+    top = np.argsort(r)[::-1][:6]
+    print(f"WE={we} N={ph.dim} prec={prec} err={np.linalg.norm(got - ref[0]):.3e} rows {top.tolist()} "
+          f"diff {[f'{x:.1e}' for x in r[top]]} ref {[f'{x:.1e}' for x in np.abs(ref[0][top])]}", flush=True)

@@ -189,7 +189,8 @@ def lib() -> ctypes.CDLL:
     L.qc_wavefunction_len.argtypes = [vp]
     L.qc_wavefunction_obs.argtypes = [vp, vp, d, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
-    L.qc_step_waves_per_env.argtypes = [vp]
+    if hasattr(L, "qc_step_waves_per_env"):   # (older in-tree builds, A/B runs: query absent)
+        L.qc_step_waves_per_env.argtypes = [vp]
     L.qc_actor_create.argtypes = [P(QcDqnParams), ctypes.c_int, P(vp)]
     L.qc_actor_destroy.argtypes = [vp]
     L.qc_actor_destroy.restype = None
@@ -223,6 +224,10 @@ def lib() -> ctypes.CDLL:
     L.qc_replay_stats.argtypes = [vp, P(QcReplayStats)]
     L.qc_replay_buffers.argtypes = [vp, P(vp), P(vp)]
     for name in EXPORTS:
+        # every declared entry point must resolve in the shipped library (a stale build fails here); an
+        # explicit QCART_LIB (A/B runs against older builds) may lack the newest ones
+        if os.environ.get("QCART_LIB") and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int:   # default
             fn.restype = ctypes.c_int

@@ -326,11 +326,9 @@ __device__ __forceinline__ char* pl_out(const PLane& p) {
 __device__ __forceinline__ const char* pl_swap(const PLane& p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __hip_atomic_store((uint32_t*)p.me, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load((const uint32_t*)p.pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < p.seq) {
-#ifdef QCART_PAIR_SLEEP
-        __builtin_amdgcn_s_sleep(QCART_PAIR_SLEEP);
-#endif
-    }
+    // (back-off between polls: s_sleep 1 measured 94 ms per C5 launch, a tight poll 108 ms)
+    while (__hip_atomic_load((const uint32_t*)p.pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < p.seq)
+        __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     return p.pa + 16 + (p.seq & 1u) * kPairData;
 }

@@ -213,12 +213,18 @@ class Stepper:
         return out
 
     def _check_actions(self, actions: torch.Tensor):
-        """int32 (B,) on the device, every value a valid slot (the reference's convert_to_force has no
-        other actions; an out-of-range one raises here instead of reaching the kernels)."""
+        """int32 (B,) on the device. The values must be valid slots (the reference's convert_to_force has no
+        other actions); that check runs on the device without a stream sync (qc_step's grouping kernel raises
+        an error word) and is reported by check(), which every synchronising method calls."""
         if actions.dtype != torch.int32 or actions.shape != (self.batch,) or actions.device != self.device:
             raise ValueError("actions must be an int32 tensor of shape (B,) on the handle's device")
-        if self.batch and bool(((actions < 0) | (actions >= self.n_slots)).any()):
-            raise ValueError(f"actions must lie in [0, {self.n_slots})")
+
+    def check(self):
+        """Raise the deferred input errors of earlier step() calls (qc_take_errors; synchronises the stream)."""
+        self._bind_stream()
+        if L.lib().qc_take_errors(self._h) != 0:
+            msg = L.lib().qc_last_error(self._h)
+            raise ValueError(f"actions must lie in [0, {self.n_slots}): {msg.decode() if msg else ''}")
 
     def wavefunction_len(self) -> int:
         return L.check(L.lib().qc_wavefunction_len(self._h), self._h)
@@ -311,7 +317,9 @@ class Stepper:
         ms, n = ctypes.c_double(), ctypes.c_int64()
         self._bind_stream()
         L.check(L.lib().qc_step_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), self._h)
+        self.check()
         return ms.value, n.value
 
     def sync(self):
         L.check(L.lib().qc_sync(self._h), self._h)
+        self.check()

@@ -59,6 +59,7 @@ struct qc_handle {
     int32_t* d_order = nullptr;   // envs grouped by force slot (step kernel with per-block LDS tables)
     size_t order_cap = 0;
     int32_t *d_kf = nullptr, *d_kb = nullptr;
+    int32_t* d_bad = nullptr;     // raised by k_group on an out-of-range action (qc_take_errors)
 };
 
 namespace {
@@ -108,6 +109,7 @@ void free_dev(qc_handle* h) {
                      &h->d_force};
     for (auto p : dp)
         if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (h->d_bad) { (void)hipFree(h->d_bad); h->d_bad = nullptr; }
     if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
     if (h->d_order) { (void)hipFree(h->d_order); h->d_order = nullptr; h->order_cap = 0; }
     if (h->d_kb) { (void)hipFree(h->d_kb); h->d_kb = nullptr; }
@@ -395,6 +397,8 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     {
         std::vector<uint64_t> zero((size_t)std::max<int64_t>(p->batch, 1), 0);
         rc = upload(h, &h->d_ctr, zero.data(), zero.size());
+        const int32_t z = 0;
+        if (!rc) rc = upload(h, &h->d_bad, &z, 1);
     }
     if (rc) {
         set_create_err(h->err);
@@ -593,7 +597,7 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             h->order_cap = cap;
         }
         if (launch_group(actions, default_action, env_steps, n_steps, h->p.batch, (int)h->acts.size(), (int)W,
-                         h->d_order, (int32_t)cap, h->stream))
+                         h->d_order, (int32_t)cap, h->d_bad, h->stream))
             return fail(h, QC_EHIP, "group kernel launch failed");
         a.order = h->d_order;
         a.n_blocks = (uint32_t)(cap / W);
@@ -801,6 +805,19 @@ int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, flo
 }
 
 int qc_step_waves_per_env(const qc_handle* h) { return h ? h->we : QC_EINVAL; }
+
+int qc_take_errors(qc_handle* h) {
+    if (!h) return QC_EINVAL;
+    DeviceGuard g(h->device);
+    int32_t v = 0;
+    if (hipMemcpyAsync(&v, h->d_bad, sizeof(v), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess)
+        return fail(h, QC_EHIP, "reading the error word failed");
+    if (!v) return QC_OK;
+    const int32_t z = 0;
+    (void)hipMemcpy(h->d_bad, &z, sizeof(z), hipMemcpyHostToDevice);
+    return fail(h, QC_EINVAL, "an action out of [0, n_slots) reached qc_step (clamped by the kernels)");
+}
 
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd) {
     if (!h || action < 0 || action >= (int)h->acts.size()) return QC_EINVAL;

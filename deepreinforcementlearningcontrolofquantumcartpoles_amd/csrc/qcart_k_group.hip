@@ -4,6 +4,8 @@
 // arbitrary and does not affect any result: envs are independent). Unused entries are -1 (idle
 // waves). Envs with no step budget this call (env_steps[e] <= 0: the reset intervals of a partly
 // finished batch) go to a last bucket of their own, so they never stretch a working workgroup.
+// An out-of-range action of an env with a step budget raises the handle's error word (bad): the step kernel
+// clamps it, and the host reports it at its next check (qc_take_errors) instead of syncing on every call.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -16,7 +18,8 @@ constexpr int kBuckets = kGroupSlots + 1;   // + the no-budget bucket (last)
 
 __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ actions, int32_t default_action,
                                                 const int32_t* __restrict__ env_steps, int32_t n_steps, int64_t B,
-                                                int n_slots, int g, int32_t* __restrict__ order, int32_t cap) {
+                                                int n_slots, int g, int32_t* __restrict__ order, int32_t cap,
+                                                int32_t* __restrict__ bad) {
     __shared__ int cnt[kBuckets], off[kBuckets], cur[kBuckets];
     __shared__ int total;
     const int t = threadIdx.x;
@@ -30,7 +33,11 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
         const int s = actions ? actions[e] : default_action;
         return s < 0 ? 0 : (s >= n_slots ? n_slots - 1 : s);
     };
-    for (int64_t e = t; e < B; e += blockDim.x) atomicAdd(&cnt[slot_of(e)], 1);
+    for (int64_t e = t; e < B; e += blockDim.x) {
+        const int s = slot_of(e);
+        if (actions && s != kGroupSlots && (actions[e] < 0 || actions[e] >= n_slots)) bad[0] = 1;
+        atomicAdd(&cnt[s], 1);
+    }
     __syncthreads();
     if (t == 0) {
         int o = 0;
@@ -51,12 +58,12 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
 }
 
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
-                 int n_slots, int gran, int32_t* order, int32_t cap, void* stream) {
+                 int n_slots, int gran, int32_t* order, int32_t cap, int32_t* bad, void* stream) {
     if (n_slots > kGroupSlots || gran < 1 ||
         (int64_t)cap < (B + gran - 1) / gran * gran + (int64_t)(gran - 1) * (n_slots + 1))
         return -1;
     hipLaunchKernelGGL(k_group, dim3(1), dim3(1024), 0, (hipStream_t)stream, actions, default_action, env_steps, n_steps,
-                       B, n_slots, gran, order, cap);
+                       B, n_slots, gran, order, cap, bad);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

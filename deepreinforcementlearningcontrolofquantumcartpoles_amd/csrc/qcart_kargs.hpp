@@ -147,6 +147,6 @@ bool have_kernel(int family, int R, int precision = 0);
 int step_waves(int family, int R, int precision = 0, int we = 1);   // envs per step-kernel workgroup (<0: none)
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
-                 int n_slots, int gran, int32_t* order, int32_t cap, void* stream);
+                 int n_slots, int gran, int32_t* order, int32_t cap, int32_t* bad, void* stream);
 
 }  // namespace qcart

@@ -252,6 +252,7 @@ class BatchedEnv:
             obs = self.rec.hist
         self.last_action = actions
         self.obs = obs
+        self.st.check()   # deferred action-range errors of this interval's step (synchronises, as done.any() does)
         if bool(done.any()):
             if self.rec is None:   # measurement mode: the rows hold the terminal record
                 info["terminal_obs"] = obs.clone()

@@ -258,6 +258,12 @@ int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bw
  * (opt-in: measured slower). */
 int qc_step_waves_per_env(const qc_handle* h);
 
+/* Deferred input errors: qc_step does not synchronise to validate its actions; an action outside
+ * [0, n_slots) of an env with a step budget raises a device error word (the kernels clamp it). This call
+ * synchronises the handle's stream, returns QC_EINVAL (message via qc_last_error) if any qc_step since the
+ * last call saw such an action, and clears the word; QC_OK otherwise. */
+int qc_take_errors(qc_handle* h);
+
 /* ---------------------------------------------------------------------------------------------
  * Batched DQN actor: the reference's direct_DQN action selection
  * (inverted harmonic oscillator/RL.py:80-111 + layers.py FactorizedNoisy / Linear_weight_normalize),

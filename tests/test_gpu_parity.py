@@ -148,6 +148,33 @@ def test_psi_parity_injected_noise(oracle_mod, name, steps, B, policy):
     assert worst < TOL_1000, worst
 
 
+# every rows-per-lane instantiation, at sizes whose row count is not a multiple of the lane count (ragged
+# padding: the grid's flushed padding rows at every N mod R, Lᵀ reads reaching 2-4 lanes ahead at R < kl),
+# with a ragged batch of 3 envs
+EDGE_SIZES = [
+    ("iho31_R1", cfg.DEFAULTS[cfg.IHO].with_(n_max=30)), ("iho101_R2", cfg.DEFAULTS[cfg.IHO].with_(n_max=100)),
+    ("iho151_R3", cfg.DEFAULTS[cfg.IHO].with_(n_max=150)), ("iho201_R4", cfg.DEFAULTS[cfg.IHO].with_(n_max=200)),
+    ("iho401_R8", cfg.DEFAULTS[cfg.IHO].with_(n_max=400)), ("iho701_R16", cfg.DEFAULTS[cfg.IHO].with_(n_max=700)),
+    ("ho41_R1", cfg.DEFAULTS[cfg.HO].with_(n_max=40)), ("ho101_R2", cfg.DEFAULTS[cfg.HO].with_(n_max=100)),
+    ("ho201_R4", cfg.DEFAULTS[cfg.HO].with_(n_max=200)), ("ho401_R8", cfg.DEFAULTS[cfg.HO].with_(n_max=400)),
+    ("qo35_R1", cfg.DEFAULTS[cfg.QO].with_(grid_size=0.5)), ("qo85_R2", cfg.DEFAULTS[cfg.QO].with_(grid_size=0.2)),
+    ("qo285_R5", cfg.DEFAULTS[cfg.QO].with_(grid_size=0.06)),
+    ("qo567_R9", cfg.DEFAULTS[cfg.QO].with_(grid_size=0.03, time_steps=5760)),
+    ("qo1063_R17", cfg.DEFAULTS[cfg.QO].with_(grid_size=0.016, time_steps=11520)),
+    ("iqo301_R5", cfg.DEFAULTS[cfg.IQO].with_(x_max=7.5)),
+]
+
+
+@pytest.mark.parametrize("name,ph", EDGE_SIZES, ids=[n for n, _ in EDGE_SIZES])
+def test_psi_parity_every_rows_per_lane(oracle_mod, name, ph):
+    """20 steps of every rows-per-lane instantiation at a ragged size and batch: psi, Fail, <x> and q equal
+    the oracle's (fp64, injected noise, random force slots)."""
+    lo, hi = (7, 13) if ph.family == cfg.IHO else (0, 20)
+    worst, alive, _ = run_pair(oracle_mod, ph, 20, 3, lo, hi, chunk=20)
+    assert alive.sum() >= 2, f"{name}: only {int(alive.sum())}/3 envs physical"
+    assert worst < 1e-11, (name, worst)
+
+
 def test_psi_parity_inkernel_philox(oracle_mod):
     """In-kernel Philox4x32-10 noise keyed by (seed, global env id, step) reproduces the oracle's."""
     ph = CASES["iho181"]

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Diagnostic: the step kernel (one wave per env, QCART_WE=1, or the wave pair) against the fp64 oracle on the
 same Philox stream from a random low-level Fock state: per-env error and the rows where it sits.
-    python tools/diag_pair.py <n_max> <precision> <B> <action|-1> <steps>"""
+    python tests/diag/diag_pair.py <n_max> <precision> <B> <action|-1> <steps>"""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, _ROOT)
+sys.path.insert(0, os.path.join(_ROOT, "tests"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

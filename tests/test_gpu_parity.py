@@ -353,6 +353,37 @@ def test_env_steps_budget_freezes_envs():
     assert not torch.equal(a[2], ref[2])
 
 
+@pytest.mark.parametrize("name", ["iho181", "ho256", "qo171", "iqo513"])
+def test_empty_inputs_and_single_env(oracle_mod, name):
+    """Edge cases of the step boundary: an empty batch (B = 0: every call is a no-op returning QC_OK, like the
+    reference's loop over no actors), zero physics steps (psi bitwise unchanged, no Fail), and a batch of one
+    env (a single partially-filled workgroup) equal to the oracle over one control interval."""
+    ph = CASES[name]
+    st0 = Stepper(ph, 0, 0, seed=3)
+    empty = st0.new_state()
+    assert empty.shape == (0, st0.N)
+    out = st0.step(empty, torch.zeros(0, dtype=torch.int32, device="cuda"), 10, want_q=True, want_obs=True)
+    assert out["fail_step"].numel() == 0 and out["q"].shape == (10, 0)
+    assert st0.moments(empty).shape[0] == 0 and st0.x_expectation(empty).numel() == 0
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = init_states(osys, ph, 1)
+    st = Stepper(ph, 1, 0, seed=3)
+    psi = torch.from_numpy(psi0.copy()).cuda()
+    acts = torch.tensor([ph.n_actions // 2 + 3], dtype=torch.int32, device="cuda")
+    out = st.step(psi, acts, 0, want_q=True)
+    torch.cuda.synchronize()
+    assert torch.equal(psi.cpu(), torch.from_numpy(psi0)) and int(out["fail_step"][0]) == 0
+    n = ph.control_interval
+    noise = np.random.default_rng(11).standard_normal((n, 1, 2))
+    ref = psi0.copy()
+    f_ref, _, xm_ref = osys.run_batch(ref, acts.cpu().numpy(), ph.f_max, n, ph.dt, ph.gamma, noise=noise,
+                                      want_q=True, n_threads=1)
+    out = st.step(psi, acts, n, noise=torch.from_numpy(noise).cuda(), want_q=True)
+    assert int(out["fail_step"][0]) == int(f_ref[0])
+    np.testing.assert_allclose(out["x_mean"].cpu().numpy(), xm_ref, atol=1e-10)
+    assert float(wnorm(ph, psi.cpu().numpy() - ref)[0]) < 1e-10
+
+
 @pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513"])
 def test_table_placements_bitwise_equal(monkeypatch, case):
     """The step kernel's factor-table placements (0: global buffer loads, 1: workgroup LDS image of

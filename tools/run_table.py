@@ -35,4 +35,5 @@ def main(tag="r01"):
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(*sys.argv[1:2])

@@ -10,7 +10,7 @@ the drivers call (IHO/main_parallel.py:174-264, IQO/main_parallel.py:123-218):
 
 Here the compile-time parameters become arguments of `load()`, which returns a module-like object
 with the same function names, signatures, return values and error behaviour; each call runs the HIP
-kernels of libqcart (B = 1) and copies the numpy state to and from the device. This surface exists
+kernels of libqcart (B = 1) and copies the numpy state to and from the device (pinned staging, one copy each way). This surface exists
 for drop-in compatibility; the throughput path is core.Stepper / env.BatchedEnv.
 
 Noise: set_seed(seed) starts the reference's stream — MT19937 seeded like vslNewStream(VSL_BRNG_MT19937,
@@ -21,15 +21,18 @@ load(..., noise="philox") selects the counter-based Philox stream instead.
 """
 from __future__ import annotations
 
+import ctypes
 import sys
 import types
 from math import pi
 
 import numpy as np
 
+from . import _lib
 from . import config as cfg
 
 _MODULES: dict = {}
+_MAX_STEPS = 10   # physics steps per drop-in call: step 1, simulate_10_steps 10
 
 
 def _check_state(state, N):
@@ -52,6 +55,8 @@ class _Simulation:
         from .core import Stepper
         if noise not in ("mt19937", "philox"):
             raise ValueError("noise must be 'mt19937' or 'philox'")
+        if physics.precision != 0:
+            raise ValueError("the drop-in computes in fp64 like the reference (precision=0)")
         self._torch = torch
         self.physics = physics
         self._noise = noise
@@ -59,9 +64,23 @@ class _Simulation:
         if noise == "mt19937":
             self._st.set_seed_mt19937(0)
         self._dev = self._st.device
-        self._psi = self._st.new_state()
         self._dt, self._gamma = physics.dt, physics.gamma
-        self.N = self._st.N
+        self.N = N = self._st.N
+        # one device block per module and its pinned host mirror: psi (2N doubles) | q [10] | x_mean [10] |
+        # Fail (int32 in one double slot). A call copies the state in through the pinned mirror and brings
+        # psi, q, x_mean and Fail back in ONE asynchronous copy, with no per-call allocation
+        self._blk_len = 2 * N + 2 * _MAX_STEPS + 1
+        self._dblk = torch.zeros(self._blk_len, dtype=torch.float64, device=self._dev)
+        self._hblk = torch.zeros(self._blk_len, dtype=torch.float64, pin_memory=True)
+        self._hnp = self._hblk.numpy()
+        self._hpsi_np = self._hnp[:2 * N].view(np.complex128)
+        self._psi = self._dblk[:2 * N].view(torch.complex128).view(1, N)
+        self._hpsi = self._hblk[:2 * N].view(torch.complex128).view(1, N)
+        base = self._dblk.data_ptr()
+        self._q_ptr = ctypes.c_void_p(base + 8 * 2 * N)
+        self._xm_ptr = ctypes.c_void_p(base + 8 * (2 * N + _MAX_STEPS))
+        self._fail_ptr = ctypes.c_void_p(base + 8 * (2 * N + 2 * _MAX_STEPS))
+        self._psi_ptr = ctypes.c_void_p(base)
 
     # set_seed(int): IHO/simulation_i.cpp:574-579
     def set_seed(self, seed):
@@ -99,19 +118,24 @@ class _Simulation:
         """n physics steps on the device; returns (q, x_mean, Fail) of the call (last step's q / x_mean;
         Fail = any step's boundary test (step) or the final state's (simulate_10_steps)). One host->device
         copy of the state and ONE device->host copy of state + the three scalars per call."""
-        _check_state(state, self.N)
+        N = self.N
+        _check_state(state, N)
         self._sync_dynamics(float(dt), float(gamma))
-        torch = self._torch
-        self._psi.copy_(torch.from_numpy(state).view(1, -1))
-        out = self._st.step(self._psi, None, n, default_action=self._slot(float(force)), want_q=True,
-                            want_fail=True)
-        fail = out["fail_step"]
+        slot = self._slot(float(force))
+        st, lib = self._st, _lib.lib()
+        np.copyto(self._hpsi_np, state)
+        self._psi.copy_(self._hpsi, non_blocking=True)
+        st._bind_stream()
+        _lib.check(lib.qc_step(st._h, self._psi_ptr, None, int(slot), int(n), None, None, self._q_ptr,
+                               self._xm_ptr, self._fail_ptr, None, None), st._h)
         if final_fail:
-            fail = self._st.boundary_fail(self._psi)
-        buf = torch.cat([self._psi.view(-1).view(torch.float64), out["q"][n - 1], out["x_mean"][n - 1],
-                         fail.to(torch.float64)]).cpu().numpy()
-        state[:] = buf[:2 * self.N].view(np.complex128)
-        return float(buf[2 * self.N]), float(buf[2 * self.N + 1]), int(buf[2 * self.N + 2] > 0)
+            _lib.check(lib.qc_boundary_fail(st._h, self._psi_ptr, self._fail_ptr), st._h)
+        self._hblk.copy_(self._dblk, non_blocking=True)
+        self._torch.cuda.current_stream(self._dev).synchronize()
+        h = self._hnp
+        state[:] = self._hpsi_np
+        fail = int(h[2 * N + 2 * _MAX_STEPS:2 * N + 2 * _MAX_STEPS + 1].view(np.int32)[0])
+        return float(h[2 * N + n - 1]), float(h[2 * N + _MAX_STEPS + n - 1]), int(fail > 0)
 
     # step(state, dt, force, gamma) -> (q, x_mean, Fail): IHO/simulation_i.cpp:358-389
     def step(self, state, dt, force, gamma):

@@ -267,8 +267,20 @@ __device__ __forceinline__ float dpp_dm(float v) {
 // rows fold up through row_bcast:15 / row_bcast:31 into lane 63, whose value is read as the one
 // (wave-uniform) total. Only lane 63's chain matters, so the broadcasts need no row mask (and no
 // zeroed destination)
+// wave issue priority experiments (s_setprio; all 0 = no instruction emitted): BASE for the step kernel,
+// SUM inside the reductions, SOLVE inside the band solve's lane scans
+#ifndef QCART_PRIO_BASE
+#define QCART_PRIO_BASE 0
+#endif
+#ifndef QCART_PRIO_SUM
+#define QCART_PRIO_SUM QCART_PRIO_BASE
+#endif
+#ifndef QCART_PRIO_SOLVE
+#define QCART_PRIO_SOLVE QCART_PRIO_BASE
+#endif
 template <int NV, typename RT>
 __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
+    if constexpr (QCART_PRIO_SUM != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SUM);
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0xb1>(v[i]);    // quad_perm [1,0,3,2]
 #pragma unroll
@@ -283,6 +295,7 @@ __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x143>(v[i]);   // rows 2, 3 += lane 31 (row_bcast:31)
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = readlane_d(v[i], 63);
+    if constexpr (QCART_PRIO_SUM != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
 }
 
 // the step kernel's reductions. (Measured and rejected: the sum on the matrix core, two
@@ -931,7 +944,9 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(10);
     if (hf) {
+        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SOLVE);
         scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf, pre);
+        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     } else {
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
@@ -1016,7 +1031,9 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(13);
     if (hb) {
+        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SOLVE);
         scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb, pre);
+        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
@@ -1212,6 +1229,7 @@ __global__ __launch_bounds__((64 * kBlockWaves<FAM, R, RT, WE>))
 __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWaves<FAM, R, RT, WE> / 4)))) void k_step(
     const KArgs a) {
     static_assert(WE == 1 || FAM == 1, "two waves per env: IHO only");
+    if constexpr (QCART_PRIO_BASE > 0) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     constexpr int KL = Fam<FAM>::KL;
     constexpr int W = kBlockWaves<FAM, R, RT, WE>;   // waves per block
     constexpr int EPB = W / WE;                       // envs per block

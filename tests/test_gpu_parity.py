@@ -56,7 +56,8 @@ CASES = {
     "iho64_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=63, gamma=0.5 * pi),
     "iho512_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=511, gamma=0.5 * pi),
     "iho512_exact_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=511, gamma=0.5 * pi, a_mode=1),
-    # N = 1024: the two-waves-per-env step kernel (R = 8 rows on each of 2 x 64 lanes)
+    # N = 1024: the largest fp64 instantiation (R = 16 rows per lane, one wave per SIMD; the opt-in
+    # QCART_WE=2 pair kernel is covered by test_pair_kernel_tracks_oracle_and_one_wave)
     "iho1024_g05": cfg.DEFAULTS[cfg.IHO].with_(n_max=1023, gamma=0.5 * pi),
     "ho256": cfg.DEFAULTS[cfg.HO].with_(n_max=255),
     "ho71": cfg.DEFAULTS[cfg.HO],

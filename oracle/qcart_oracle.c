@@ -1,6 +1,6 @@
 /*
  * qcart_oracle.c — TEST INFRASTRUCTURE ONLY: CPU fp64 restatement of the reference stepper.
- * See qcart_oracle.h for scope and PARITY STATUS (unpinned vs the reference binary; pinned by KATs).
+ * See qcart_oracle.h for scope and PARITY STATUS (pinned at the reference's MKL boundary and by KATs; the binary never ran).
  *
  * Every function cites the reference file:line it restates. Aliases:
  *   HO/  = implementation codes/harmonic oscillator/

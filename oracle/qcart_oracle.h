@@ -8,12 +8,16 @@
  *   QO  = quartic oscillator/simulation_quart.cpp (byte-identical to the IQO copy)
  * plus the Python-side observation / termination / reset helpers of each family main_parallel.py.
  *
- * PARITY STATUS: parity against the reference binary is UNPINNED. Compiling or running the
- * reference extension was denied in this environment and the reference ships no
- * golden vectors or tests. This restatement is pinned instead by physics
+ * PARITY STATUS: pinned at the reference's MKL boundary; the reference binary itself never ran.
+ * Compiling or running the reference extension was denied in this environment and
+ * the reference ships no golden vectors or tests. The MKL 2021.4 runtime the reference
+ * links is driven through ctypes in the reference's call order and descriptors (tests/golden/mklref.py,
+ * make_mkl_fixtures.py -> mkl_v1.npz): this restatement equals it (tests/test_mkl_fixtures.py: MT19937
+ * words bit for bit, Box-Muller <= 2 ulp, zgbtrf pivots / zgbtrs solves, the HERMITIAN-descriptor term7,
+ * the DIAG_UNIT p relative, 1000-step MKL-ordered trajectories to 1e-9). Also pinned by physics
  * known-answer tests (tests/test_oracle_kat.py: dense-numpy operators built from the reference's
  * own Python operator definitions, unitary expm propagation, Gaussian moments, norm, pivot-free LU)
- * and by the committed fixtures it generated (tests/golden/).
+ * and guarded against drift by the committed fixtures it generated (tests/golden/golden_v1.npz).
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
  */

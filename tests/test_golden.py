@@ -1,7 +1,7 @@
 """CPU: the oracle reproduces the committed golden fixtures (tests/golden/golden_v1.npz, made by
 tests/golden/make_golden.py). Guards the checker itself against drift; the GPU path is held to the
-same fixtures in tests/test_gpu_golden.py. Parity vs the reference binary remains unpinned
-(SURVEY.md §8c)."""
+same fixtures in tests/test_gpu_golden.py. Reference parity is pinned separately, at the
+reference's MKL boundary (tests/test_mkl_fixtures.py)."""
 import os
 
 import numpy as np

@@ -2,7 +2,7 @@
 inputs and identical Wiener noise.
 
 Tolerance (BASELINE.json north_star): ||psi_GPU - psi_ref||_2 < 1e-9 after 1000 steps, fp64.
-The oracle is the checker only (parity vs the reference binary itself is unpinned, see
+The oracle is the checker only; it is pinned at the reference's MKL boundary (tests/test_mkl_fixtures.py,
 oracle/qcart_oracle.h).
 """
 from math import pi, sqrt

@@ -1,7 +1,7 @@
 """Pin the CPU restatement (oracle/) with known-answer tests.
 
-Parity against the reference binary is unpinned (running it is denied; the reference
-has no tests or fixtures, §4). These tests pin the restatement against independent physics and
+The reference binary never ran (denied; the reference has no tests or fixtures, §4); its
+MKL boundary is pinned in tests/test_mkl_fixtures.py. These tests pin the restatement against independent physics and
 against dense numpy restatements of the reference's own Python operator definitions.
 """
 from math import pi, sqrt

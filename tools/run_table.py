@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""BASELINE.md §4 run table from the per-config bench lines (profiles/r01_<cfg>_bench_line.json) and
-rocprofv3 summaries (profiles/r01_<cfg>_summary.json) written by tools/run_table.sh + prof_summary.py.
-Prints a markdown table and writes profiles/r01_run_table.json."""
+"""BASELINE.md §4 run table from the per-config bench lines (profiles/<tag>_<cfg>_bench_line.json) and
+rocprofv3 summaries (profiles/<tag>_<cfg>_summary.json) written by tools/run_table.sh + prof_summary.py.
+Prints a markdown table and writes profiles/<tag>_run_table.json.  python tools/run_table.py [tag]"""
 import json
 import os
 

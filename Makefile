@@ -5,7 +5,7 @@ CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
 OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o)
-HDRS := include/qcart.h $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
+HDRS := include/qcart.h $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
 all: $(LIB) oracle
 
@@ -36,7 +36,7 @@ clean:
 
 .PHONY: all oracle clean resource-usage expt expt_actor
 
-# experiment builds (not shipped): make expt EXPT=-DQCART_EXPT_NOLOAD NAME=noload [TU=qcart_k_grid]
+# experiment builds (not shipped): make expt EXPT=-DQCART_STAMPS NAME=stamps [TU=qcart_k_grid]
 EXPT ?=
 NAME ?= expt
 TU ?= qcart_k_iho

@@ -84,7 +84,18 @@ def cpu_baseline(config: str, seconds: float, threads: int):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def latest_profile(workload: str):
+def lib_sha() -> str:
+    """sha256 (16 hex digits) of the libqcart.so this run loads: a committed profile's traffic is only
+    reported for the exact library it was measured on."""
+    import hashlib
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def latest_profile(workload: str, sha: str):
+    """The newest committed rocprofv3 summary (profiles/*_summary.json, tools/prof_summary.py) whose
+    profiled bench line ran this workload on this same library build and whose kernel is a k_step."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
@@ -93,7 +104,8 @@ def latest_profile(workload: str):
         except Exception:
             continue
         bl = d.get("bench_line") or {}
-        if bl.get("config", {}).get("workload") == workload and "hbm_bytes_per_launch" in d:
+        if (bl.get("config", {}).get("workload") == workload and "hbm_bytes_per_launch" in d
+                and bl.get("roofline", {}).get("lib_sha") == sha and "k_step" in d.get("kernel", "")):
             best = d
     return best
 
@@ -115,6 +127,9 @@ def dry_run(world: int, rank: int):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    # under a launcher (WORLD_SIZE set, world 1 included) the ranks form an RCCL group; a plain
+    # `python bench.py` (N = 1) runs without one
+    use_dist = world > 0
     if world == 0:
         if args.gpus > 1:
             sys.exit(launch_ranks(args.gpus))
@@ -130,15 +145,14 @@ def main():
     import torch.distributed as dist
 
     from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import distributed as D
     from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper
 
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if use_dist:
+        D.init_from_env("nccl")              # RCCL (torch.distributed "nccl" on ROCm), one rank per GPU
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if use_dist else 0)
 
     conf = cfg.BENCH_CONFIGS[args.config]
     ph = conf["physics"]
@@ -164,7 +178,7 @@ def main():
     for k in range(args.warmup):
         one(k)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     st.set_timing(True)          # HIP events around each k_step launch, on the stream it runs on
@@ -172,7 +186,7 @@ def main():
     for k in range(args.steps):
         out = one(args.warmup + k)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -181,14 +195,18 @@ def main():
     kern_ms = kern_total / max(launches, 1)
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     world_seen = 1
-    if world > 1:
+    rccl = None
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         world_seen = dist.get_world_size()
-        # RCCL gather of per-env episode statistics (here: survival flags of this control step)
-        alive = (out["fail_step"] == 0).to(torch.float64).sum().reshape(1)
-        gathered = [torch.zeros_like(alive) for _ in range(world)]
-        dist.all_gather(gathered, alive)
+        # RCCL gather of per-env episode statistics after the timed region (distributed.gather_episode_stats,
+        # device tensors): each env's survival through the last control step and its first Fail step
+        survived = (out["fail_step"] == 0).to(torch.float64)
+        R, L = D.gather_episode_stats(survived, out["fail_step"].to(torch.float64))
+        rccl = {"backend": dist.get_backend(), "world_size": world_seen, "gathered_envs": int(R.numel()),
+                "gathered_survivors": float(R.sum().item()), "device": str(R.device)}
     elapsed, kern_ms = float(t[0]), float(t[1])
+    sha = lib_sha()
     units = B * world * n_sub * args.steps
     value = units / elapsed
     N = ph.dim
@@ -213,26 +231,29 @@ def main():
         "data": ("synthetic (random psi0 on Fock levels < 16; actions ~ U{0..20} per control step)" if ph.fock else
                  "synthetic (Gaussian packets mu~U[-1,1], sigma~U[0.7,1.3], k~U[-0.3,0.3]; actions ~ U{0..20} "
                  "per control step)"),
-        "config": {"workload": f"{cfg.FAMILY_NAMES[ph.family]} N={N} per-GPU batch={B} "
+        "config": {"workload": f"{cfg.FAMILY_NAMES[ph.family]} N={N} per-GPU batch={B} dt=1/{ph.time_steps} "
                                f"{n_sub} physics steps + moments per step ({args.config})",
                    "global_batch": B * world, "seq_len": N, "parallelism": f"env-shard{world}",
-                   "physics_steps_per_step": n_sub, "world_size_seen": world_seen},
-        # what bounds k_step is the FP vector pipe (psi stays in VGPRs across the fused steps); achieved /
-        # frac are the north-star yardstick: algorithmic psi bytes (read + write per physics step) / time
-        "roofline": {"bound": "fp32_valu" if fp32 else "fp64_valu", "achieved": achieved / 1e9,
-                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
+                   "physics_steps_per_step": n_sub, "world_size_seen": world_seen, "rccl": rccl},
+        # bound / achieved / peak / frac: the north-star HBM yardstick — algorithmic psi bytes (read + write
+        # per physics step) per k_step launch / the launch's time, against the HBM peak. What actually binds
+        # k_step is the FP vector pipe (psi stays in VGPRs across the fused steps): that roofline is the
+        # separate "binding" object, in TFLOP/s against the FP64 (FP32 for C5) vector peak
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM, "traffic": None,
                      "yardstick": f"{int(bpe)}*N B/env-step (psi read+write) x env-steps per launch / k_step time "
                                   "(SURVEY §8d north-star yardstick; the kernel keeps psi on chip, measured_gbs is "
                                   "the real HBM traffic rate)",
                      "kernel": "k_step", "kernel_ms": kern_ms, "kernel_launches": launches,
-                     "valu_frac": flops / peak_valu},
+                     "lib_sha": sha,
+                     "binding": {"bound": "fp32_valu" if fp32 else "fp64_valu", "achieved": flops / 1e12,
+                                 "peak": peak_valu / 1e12, "unit": "TFLOP/s", "frac": flops / peak_valu,
+                                 "flops_per_elem": FLOPS_PER_ELEM[ph.family]}},
         "rl_steps_per_s": value / ph.control_interval,
-        "valu": {"achieved_tflops": flops / 1e12, "peak_tflops": peak_valu / 1e12,
-                 "frac": flops / peak_valu, "flops_per_elem": FLOPS_PER_ELEM[ph.family]},
     }
     # HBM traffic per launch measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, tools/prof_summary.py)
     # for this same workload, when a committed profile exists
-    prof = latest_profile(res["config"]["workload"])
+    prof = latest_profile(res["config"]["workload"], sha)
     if prof is not None:
         res["roofline"]["traffic"] = prof["hbm_bytes_per_launch"]
         res["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC, profiles/%s_summary.json)" % prof["tag"]
@@ -245,7 +266,7 @@ def main():
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -92,7 +92,10 @@ DEFAULTS = {
 BENCH_CONFIGS = {
     "C1": dict(physics=DEFAULTS[HO].with_(n_max=255), batch=1),
     "C2": dict(physics=DEFAULTS[IHO].with_(n_max=511), batch=4096),
-    "C3": dict(physics=DEFAULTS[QO].with_(x_max=8.5, grid_size=8.5 / 512), batch=16384),
+    # C3's fine grid (h = 8.5/512) is only stable for dt <= 1/11520: at the driver's 1/1440 every env Fails
+    # within 1000 steps (oracle alike, tests/test_gpu_parity.py), so the workload runs at the stable dt
+    # (control interval 640 physics steps)
+    "C3": dict(physics=DEFAULTS[QO].with_(x_max=8.5, grid_size=8.5 / 512, time_steps=11520), batch=16384),
     "C4": dict(physics=DEFAULTS[IQO].with_(x_max=12.8, grid_size=0.05), batch=65536),
     "C5": dict(physics=DEFAULTS[IHO].with_(n_max=2047, precision=1), batch=262144),
     "metric": dict(physics=DEFAULTS[IHO].with_(n_max=511), batch=65536),

@@ -230,7 +230,8 @@ class Stepper:
         return L.check(L.lib().qc_wavefunction_len(self._h), self._h)
 
     def wavefunction_obs(self, psi: torch.Tensor, input_scaling: float = 1.0) -> torch.Tensor:
-        """get_data_wavefunction(state) * input_scaling (float32 [B][2 (N - 20)], qc_wavefunction_obs)."""
+        """get_data_wavefunction(state) * input_scaling (float32 [B][wavefunction_len()]: HO state[:-10], IHO
+        state[:-20], grid state[10:-10]; qc_wavefunction_obs)."""
         self._check_psi(psi)
         out = torch.empty((self.batch, self.wavefunction_len()), dtype=torch.float32, device=self.device)
         self._bind_stream()

@@ -775,6 +775,7 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
     a.reward = reward;
     a.B = h->p.batch;
     a.n_slots = (int32_t)h->acts.size();
+    a.bad = h->d_bad;
     a.L = read_length;
     a.cg = coarse_grain;
     a.m = n_steps / coarse_grain;
@@ -788,18 +789,27 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
     return rc ? fail(h, rc, "record kernel launch failed") : QC_OK;
 }
 
+// the rows get_data_wavefunction keeps: HO state[:-10] (HO/main_parallel.py:132-134), IHO state[:-20]
+// (IHO/main_parallel.py:133-135), grid state[10:-10] (QO/main_parallel.py:132-133, IQO:136-137)
+static int wavefunction_rows(const qc_handle* h, int* lo) {
+    *lo = h->op.fock ? 0 : 10;
+    return h->op.N - (h->op.family == QC_HO ? 10 : 20);
+}
+
 int qc_wavefunction_len(const qc_handle* h) {
     if (!h) return QC_EINVAL;
-    return 2 * (h->op.N - 20);   // Fock state[:-20], grid state[10:-10]
+    int lo;
+    return 2 * wavefunction_rows(h, &lo);
 }
 
 int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, float* out) {
     if (!h) return QC_EINVAL;
     if (h->p.batch > 0 && (!psi || !out)) return fail(h, QC_EINVAL, "psi and out are required");
-    if (h->op.N <= 20) return fail(h, QC_EINVAL, "the wavefunction input needs N > 20");
+    int lo;
+    const int rows = wavefunction_rows(h, &lo);
+    if (rows <= 0) return fail(h, QC_EINVAL, "the wavefunction input needs more rows than it drops");
     DeviceGuard g(h->device);
-    const int lo = h->op.fock ? 0 : 10;
-    int rc = launch_wavefunction(psi, h->p.precision, h->p.batch, h->op.N, lo, h->op.N - 20, input_scaling, out,
+    int rc = launch_wavefunction(psi, h->p.precision, h->p.batch, h->op.N, lo, rows, input_scaling, out,
                                  h->stream);
     return rc ? fail(h, QC_EHIP, "wavefunction kernel launch failed") : QC_OK;
 }

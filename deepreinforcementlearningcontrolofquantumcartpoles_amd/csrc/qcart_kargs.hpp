@@ -118,6 +118,7 @@ struct RecArgs {
     const float* reward;        // [B] or null
     int64_t B;
     int32_t n_slots;            // action slots (out-of-range actions clamp like k_step's)
+    int32_t* bad;               // the handle's error word: raised on an out-of-range action (qc_take_errors)
     int32_t L, m, K, cg, row_len;
     int32_t vec4;               // L, m multiples of 4: float4 history traffic
     double scaling;

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qcart_expt.hpp"
 #include "qcart_kargs.hpp"
 
 namespace qcart {
@@ -143,12 +144,6 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
 __device__ __forceinline__ double u2d(unsigned lo, unsigned hi) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-#ifdef QCART_EXPT_NOLOAD   // latency experiment only: results are wrong
-template <typename RT>
-__device__ __forceinline__ cx<RT> bld_c(rsrc_t, int voff, int soff) { return C(RT(1e-3) * (RT)((voff + soff) & 7), RT(1e-4)); }
-template <typename RT>
-__device__ __forceinline__ RT bld_d(rsrc_t, int voff, int soff) { return RT(1e-6) * (RT)((voff + soff) & 7); }
-#else
 template <typename RT>
 __device__ __forceinline__ cx<RT> bld_c(rsrc_t r, int voff, int soff) {
     if constexpr (sizeof(RT) == 8) {
@@ -168,27 +163,7 @@ __device__ __forceinline__ RT bld_d(rsrc_t r, int voff, int soff) {
         return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
     }
 }
-#endif
 
-// Diagnostic build only (-DQCART_STAMPS): per-phase cycle shares of the step loop, summed over all
-// waves into qc_stamps[] (read back by qc_debug_stamps). No stamp executes in the shipped build.
-#ifdef QCART_STAMPS
-__device__ unsigned long long qc_stamps[16];
-#define QC_STAMP(ph)                                                                                 \
-    do {                                                                                             \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        unsigned long long t_;                                                                       \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        st_acc[st_ph] += t_ - st_t;                                                                  \
-        st_t = t_;                                                                                   \
-        st_ph = (ph);                                                                                \
-    } while (0)
-#else
-#define QC_STAMP(ph) \
-    do {             \
-    } while (0)
-#endif
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -267,20 +242,8 @@ __device__ __forceinline__ float dpp_dm(float v) {
 // rows fold up through row_bcast:15 / row_bcast:31 into lane 63, whose value is read as the one
 // (wave-uniform) total. Only lane 63's chain matters, so the broadcasts need no row mask (and no
 // zeroed destination)
-// wave issue priority experiments (s_setprio; all 0 = no instruction emitted): BASE for the step kernel,
-// SUM inside the reductions, SOLVE inside the band solve's lane scans
-#ifndef QCART_PRIO_BASE
-#define QCART_PRIO_BASE 0
-#endif
-#ifndef QCART_PRIO_SUM
-#define QCART_PRIO_SUM QCART_PRIO_BASE
-#endif
-#ifndef QCART_PRIO_SOLVE
-#define QCART_PRIO_SOLVE QCART_PRIO_BASE
-#endif
 template <int NV, typename RT>
 __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
-    if constexpr (QCART_PRIO_SUM != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SUM);
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0xb1>(v[i]);    // quad_perm [1,0,3,2]
 #pragma unroll
@@ -295,7 +258,6 @@ __device__ __forceinline__ void wave_sum(RT (&v)[NV]) {
     for (int i = 0; i < NV; ++i) v[i] += dpp_d<0x143>(v[i]);   // rows 2, 3 += lane 31 (row_bcast:31)
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = readlane_d(v[i], 63);
-    if constexpr (QCART_PRIO_SUM != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
 }
 
 // the step kernel's reductions. (Measured and rejected: the sum on the matrix core, two
@@ -894,13 +856,6 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
         for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], P[i * KL + k], c[k]);
 }
 
-#ifdef QCART_STAMPS
-#define QC_SOLVE_STAMP_ARGS , unsigned long long (&st_acc)[16], unsigned long long& st_t, int& st_ph
-#define QC_SOLVE_STAMP_PASS , st_acc, st_t, st_ph
-#else
-#define QC_SOLVE_STAMP_ARGS
-#define QC_SOLVE_STAMP_PASS
-#endif
 // Composite level offsets: forward level l at f0 + l*C, row prefix at fP; backward at b0 + l*C, bP
 // (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
 // SYM (grid): the backward factor U[r][r+1+k] / U[r][r] is read as L[r+1+k][r] from the lc band (row
@@ -944,9 +899,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(10);
     if (hf) {
-        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SOLVE);
         scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf, pre);
-        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     } else {
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
@@ -1031,9 +984,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(13);
     if (hb) {
-        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_SOLVE);
         scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb, pre);
-        if constexpr (QCART_PRIO_SOLVE != QCART_PRIO_BASE) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
@@ -1229,7 +1180,6 @@ __global__ __launch_bounds__((64 * kBlockWaves<FAM, R, RT, WE>))
 __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWaves<FAM, R, RT, WE> / 4)))) void k_step(
     const KArgs a) {
     static_assert(WE == 1 || FAM == 1, "two waves per env: IHO only");
-    if constexpr (QCART_PRIO_BASE > 0) __builtin_amdgcn_s_setprio(QCART_PRIO_BASE);
     constexpr int KL = Fam<FAM>::KL;
     constexpr int W = kBlockWaves<FAM, R, RT, WE>;   // waves per block
     constexpr int EPB = W / WE;                       // envs per block
@@ -1386,11 +1336,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
-#ifdef QCART_STAMPS
-    unsigned long long st_acc[16] = {0}, st_t = 0;
-    int st_ph = 9;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");
-#endif
+    QC_STAMP_BEGIN();
     for (int k = 0; k < n_my; ++k) {
         QC_STAMP(0);
         if ((k & 63) == 0) {   // lane j: normals of step k + j
@@ -1806,11 +1752,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
         }
         }   // Fock families
     }
-#ifdef QCART_STAMPS
-    QC_STAMP(9);
-    if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(&qc_stamps[i], st_acc[i]);
-#endif
+    QC_STAMP_END(lane);
     if constexpr (RCL) load_coef<FAM, R>(cf, a, base);   // x_r for grid_obs (not held across the loop)
     // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
     // across the loop)
@@ -1827,7 +1769,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
     if (lane == 0 && half == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;
-        a.ctr[env] = ctr0 + (uint64_t)n_my;
+        if (!a.noise) a.ctr[env] = ctr0 + (uint64_t)n_my;   // only the in-kernel Philox stream advances
     }
     if (a.obs_out) {
         if constexpr (FAM <= 1) {
@@ -2187,12 +2129,3 @@ int launch_f32(int family, int R, int kind, const KArgs& a, int what, double xth
 
 }  // namespace qcart
 
-#ifdef QCART_STAMPS
-// diagnostic build: read and clear the per-phase cycle sums of the step kernel of the translation unit built
-// with -DQCART_STAMPS (weak: an experiment build stamps one family TU)
-extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qcart::qc_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    unsigned long long z[16] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(qcart::qc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif

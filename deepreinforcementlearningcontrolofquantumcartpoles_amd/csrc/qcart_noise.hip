@@ -13,10 +13,15 @@
 //     the AVX-512 and AVX2 paths differ by up to 1e-8, both within 5e-8 of the exact formula); under
 //     MKL_CBWR=COMPATIBLE it is the formula above to <= 2 ulp, which this kernel (fp64 ocml log / sin)
 //     reproduces.
+//   * a first word of 0 (u1 = 0, probability 2^-32 per normal) does not give MKL an infinite normal: its
+//     Box–Muller returns sqrt(-2 ln u1) = 3.4244955099270222 for it on every code path (a state with a
+//     planted zero word loaded by vslLoadStreamM, tests/golden/mkl_v2.npz "zero/*"), so that radius is used.
 // The states live in HBM ([B][kMtWords] uint32: 624 words + the read index) and advance only by the
 // words an env actually consumes (2 normals per step it takes), exactly as each reference actor's
 // stream does.
 #include <hip/hip_runtime.h>
+
+constexpr double kMklZeroWordRadius = 3.4244955099270222;   // MKL 2021.4 BOXMULLER at u1 = 0
 
 #include <stdint.h>
 
@@ -114,9 +119,12 @@ __global__ __launch_bounds__(256) void k_mt_normals(uint32_t* st, int64_t B, int
         }
         const int avail = (int)((need - done) < (int64_t)(kN - idx) ? (need - done) : (int64_t)(kN - idx));
         for (int p = lane; p < avail / 2; p += 64) {
-            const double u1 = (double)temper(mt[idx + 2 * p]) * 0x1.0p-32;
+            const uint32_t w1 = temper(mt[idx + 2 * p]);
+            const double u1 = (double)w1 * 0x1.0p-32;
             const double u2 = (double)temper(mt[idx + 2 * p + 1]) * 0x1.0p-32;
-            const double x = sqrt(-2.0 * log(u1)) * sin(6.283185307179586 * u2);
+            // a zero first word: MKL returns the finite radius kMklZeroWordRadius, not inf (pinned, below)
+            const double rad = w1 ? sqrt(-2.0 * log(u1)) : kMklZeroWordRadius;
+            const double x = rad * sin(6.283185307179586 * u2);
             const int64_t n = done / 2 + p;   // normal index of the env: step n / 2, component n % 2
             noise[((size_t)(n >> 1) * B + e) * 2 + (n & 1)] = x;
         }

@@ -44,7 +44,12 @@ __global__ __launch_bounds__(kRecThreads) void k_record(const RecArgs a) {
     for (int j = tid; j < K + 1; j += kRecThreads) sf[j] = fresh ? 0.f : frc[j];
     __syncthreads();
     int slot = a.actions ? a.actions[env] : a.default_action;
-    slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // as k_step (the host validates)
+    // an out-of-range action raises the handle's error word (reported by the next qc_take_errors, like
+    // qc_step's) and is clamped so no table is indexed past its end
+    if (slot < 0 || slot >= a.n_slots) {
+        if (tid == 0 && a.bad) a.bad[0] = 1;
+        slot = slot < 0 ? 0 : a.n_slots - 1;
+    }
     const double f = a.slot_force[slot];
     const float fs = (float)(f * a.scaling);   // force * args.input_scaling (IHO:266, :288)
     const int64_t B = a.B;

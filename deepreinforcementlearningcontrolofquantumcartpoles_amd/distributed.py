@@ -27,11 +27,13 @@ def shard(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
-    """Initialise the default process group from torchrun's env (127.0.0.1 rendezvous)."""
+    """Initialise the default process group from torchrun's env (127.0.0.1 rendezvous) whenever a
+    launcher set WORLD_SIZE — world 1 included, so a one-GPU run under a launcher still goes through
+    RCCL (the fake-cluster case of SURVEY §4 item 4). Without WORLD_SIZE nothing is initialised."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if "WORLD_SIZE" in os.environ and not dist.is_initialized():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -45,8 +47,9 @@ def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
 
 def gather_episode_stats(returns: torch.Tensor, lengths: torch.Tensor, group=None):
     """All-gather variable-length per-rank episode (return, length) vectors; every rank gets the
-    concatenation in rank order. One small all_gather of counts + one of the padded payloads."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    concatenation in rank order. One small all_gather of counts + one of the padded payloads (also at
+    world 1 when a process group exists: the collective path is the one that runs)."""
+    if not (dist.is_available() and dist.is_initialized()):
         return returns.to(torch.float64), lengths.to(torch.float64)
     world = dist.get_world_size(group)
     dev = returns.device

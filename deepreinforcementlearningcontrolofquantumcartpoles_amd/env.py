@@ -17,8 +17,9 @@ Reference semantics reproduced per family ('xp' observation input):
         otherwise the episode ends without storing it; the episode is truncated at t_max = 100
 The experience row layout is the reference's: [last_obs, obs, last_action, reward]
 (IHO/main_parallel.py:250-257), so the deep-Q consumer drops in unchanged. With input='wavefunction'
-the observation is get_data_wavefunction(state) * input_scaling: float32 hstack(Re, Im) of state[:-20]
-(Fock, IHO/main_parallel.py:133-135) or state[10:-10] (grid, IQO/main_parallel.py:136-137)
+the observation is get_data_wavefunction(state) * input_scaling: float32 hstack(Re, Im) of state[:-10]
+(HO, HO/main_parallel.py:132-134), state[:-20] (IHO, IHO/main_parallel.py:133-135) or state[10:-10]
+(grid, IQO/main_parallel.py:136-137)
 (qc_wavefunction_obs). With input='measurements'
 (HO, IHO; IHO/main_parallel.py:143-151,270-309) the observation is the device measurement record
 [B][2][read_length] (measurements.MeasurementRecord, updated in place by the qc_record kernel) and the

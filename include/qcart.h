@@ -190,8 +190,9 @@ int qc_energy(qc_handle* h, const void* psi, double* out);
 /* phonon_number(state) (HO/main_parallel.py:88-89, harmonic-cooling reward) = sum n |psi_n|^2: out [B] */
 int qc_phonon_number(qc_handle* h, const void* psi, double* out);
 
-/* get_data_wavefunction (args.input == 'wavefunction'): hstack(Re, Im) of state[:-20] (Fock,
- * IHO/main_parallel.py:133-135) or state[10:-10] (grid, IQO/main_parallel.py:136-137), cast to float32 and
+/* get_data_wavefunction (args.input == 'wavefunction'): hstack(Re, Im) of state[:-10] (HO,
+ * HO/main_parallel.py:132-134), state[:-20] (IHO, IHO/main_parallel.py:133-135) or state[10:-10] (grid,
+ * QO/main_parallel.py:132-133, IQO/main_parallel.py:136-137), cast to float32 and
  * times input_scaling in float32 (IHO:241,247): out [B][qc_wavefunction_len()] float32 (device) */
 int qc_wavefunction_len(const qc_handle* h);
 int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, float* out);
@@ -242,7 +243,9 @@ int qc_control(qc_handle* h, const void* psi, int32_t strategy, double con_param
  * experience row hstack(measurements_input[::-1] (read_length + m), forces_to_store[::-1] (K + 1),
  * last_action, reward) (IHO:279-283, TrainDQN reads it at RL.py:180-192); the reward column is written
  * only when reward [B] is given. The drivers' values: read_length = round(n_periods * 2 * 1440) with
- * n_periods 2 (IHO, 5760) or 1.5 (HO, 4320), coarse_grain = time_steps / 1440. */
+ * n_periods 2 (IHO, 5760) or 1.5 (HO, 4320), coarse_grain = time_steps / 1440. An out-of-range action
+ * is clamped on the device and raises the handle's error word: the next qc_take_errors reports it (as for
+ * qc_step). */
 int qc_record_row_len(int32_t read_length, int32_t interval, int32_t coarse_grain);
 int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double input_scaling, const double* q,
               int32_t n_steps, const int32_t* actions, int32_t default_action, const uint8_t* mode, float* hist,

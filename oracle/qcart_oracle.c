@@ -858,9 +858,13 @@ uint32_t qo_mt_next(uint32_t* st) {
 }
 void qo_mt_normals(uint32_t* st, int64_t n, double* out) {
     for (int64_t i = 0; i < n; i++) {
-        double u1 = (double)qo_mt_next(st) * 0x1.0p-32;
+        uint32_t w1 = qo_mt_next(st);
+        double u1 = (double)w1 * 0x1.0p-32;
         double u2 = (double)qo_mt_next(st) * 0x1.0p-32;
-        out[i] = sqrt(-2. * log(u1)) * sin(6.283185307179586 * u2);
+        /* u1 = 0: MKL's BOXMULLER returns the finite radius 3.4244955099270222 (measured with a planted
+         * zero word, tests/golden/mkl_v2.npz zero/ *), not inf */
+        double rad = w1 ? sqrt(-2. * log(u1)) : 3.4244955099270222;
+        out[i] = rad * sin(6.283185307179586 * u2);
     }
 }
 

@@ -1,5 +1,8 @@
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -7,10 +10,42 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+RCCL_BATCH = 512
+
+
+def _selects_gpu(config) -> bool:
+    m = (config.getoption("markexpr", "") or "").replace(" ", "")
+    return "gpu" in m and "notgpu" not in m
+
+
+def _start_rccl_child(config):
+    """tests/test_gpu_rccl.py: bench.py's rank body under a launcher's environment at WORLD_SIZE = 1 (an RCCL
+    communicator of one rank). Started here, before collection imports any module that initialises the GPU
+    in this process, so the child is a fresh program started by a process that never touched the GPU."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = tempfile.NamedTemporaryFile(prefix="qcart_rccl_", suffix=".log", delete=False)
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = ["timeout", "-k", "10", "300", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1",
+           "--steps", "3", "--warmup", "1", "--batch", str(RCCL_BATCH), "--no-cpu-baseline"]
+    proc = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=out, stderr=subprocess.STDOUT)
+    config._qcart_rccl = (proc, out.name)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    if _selects_gpu(config) and os.path.exists("/dev/kfd"):
+        _start_rccl_child(config)
+
+
+def pytest_unconfigure(config):
+    h = getattr(config, "_qcart_rccl", None)
+    if h is not None and h[0].poll() is None:
+        h[0].kill()
+        h[0].wait()
 
 
 @pytest.fixture(scope="session")

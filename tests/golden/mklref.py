@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from math import sqrt
+from math import pi, sqrt
 
 import numpy as np
 
@@ -78,12 +78,17 @@ def mkl():
         m.cblas_dznrm2.restype = d
         m.cblas_zdscal.argtypes = [i, d, vp, i]
         m.cblas_daxpy.argtypes = [i, d, vp, i, vp, i]
+        m.cblas_dcopy.argtypes = [i, vp, i, vp, i]
+        m.cblas_dscal.argtypes = [i, d, vp, i]
         m.cblas_zcopy.argtypes = [i, vp, i, vp, i]
         m.MKL_Set_Num_Threads.argtypes = [i]
         m.vslNewStream.argtypes = [P(vp), i, ctypes.c_uint]
         m.vslDeleteStream.argtypes = [P(vp)]
         m.viRngUniformBits.argtypes = [i, vp, i, vp]
         m.vdRngGaussian.argtypes = [i, vp, i, vp, d, d]
+        m.vslGetStreamSize.argtypes = [vp]
+        m.vslSaveStreamM.argtypes = [vp, vp]
+        m.vslLoadStreamM.argtypes = [P(vp), vp]
         m.MKL_Set_Num_Threads(1)   # mkl_set_num_threads(1), IHO/simulation_i.cpp:15-16
         _mkl = m
     return _mkl
@@ -229,6 +234,39 @@ def vsl_gaussian(seed: int, n: int) -> np.ndarray:
     return out
 
 
+# MT19937 stream memory (vslSaveStreamM, MKL 2021.4): 32-bit words 5..628 are mt19937ar's state array, word
+# 629 its read index (the next output is temper(mt[index]); 624 = a twist is due) — found by comparing the
+# saved memory with mt19937ar at several positions
+_MT_OFF, _MT_IDX = 5, 629
+
+
+def vsl_planted_zero(seed: int, k: int, zero_at, n_normals: int):
+    """The stream of `seed` after k words with the state words at positions k + z (z in zero_at) set to 0
+    (their tempered output is then 0), loaded back by vslLoadStreamM: returns (state [625] = mt[624] +
+    index, the same layout as the oracle's MT19937.st, and the next n_normals vdRngGaussian(BOXMULLER)
+    normals, drawn 2 per call like the reference)."""
+    m = mkl()
+    s = vsl_stream(seed)
+    if k:
+        buf = np.zeros(k, np.uint32)
+        _ok(m.viRngUniformBits(0, s, k, _p(buf)), "viRngUniformBits")
+    mem = np.zeros(m.vslGetStreamSize(s), np.uint8)
+    _ok(m.vslSaveStreamM(s, _p(mem)), "vslSaveStreamM")
+    m.vslDeleteStream(ctypes.byref(s))
+    w = mem[: len(mem) // 4 * 4].view(np.uint32)
+    assert 0 < k < 624 and int(w[_MT_IDX]) == k and all(k + z < 624 for z in zero_at)
+    for z in zero_at:
+        w[_MT_OFF + k + z] = 0
+    state = np.concatenate([w[_MT_OFF:_MT_OFF + 624], w[_MT_IDX:_MT_IDX + 1]]).copy()
+    s2 = ctypes.c_void_p()
+    _ok(m.vslLoadStreamM(ctypes.byref(s2), _p(mem)), "vslLoadStreamM")
+    out = np.zeros(n_normals, np.float64)
+    for j in range(0, n_normals, 2):
+        _ok(m.vdRngGaussian(GAUSS_BOXMULLER, s2, 2, _p(out[j:]), 0.0, 1.0), "vdRngGaussian")
+    m.vslDeleteStream(ctypes.byref(s2))
+    return state, out
+
+
 # -------------------------------------------------------------------------------------- IHO stepper
 class IhoMkl:
     """The inverted-harmonic `simulation` module (N_MAX = n_max, OMEGA = omega) in its own MKL calls."""
@@ -237,6 +275,8 @@ class IhoMkl:
         self.n_max, self.N, self.omega = n_max, n_max + 1, omega
         n = self.N
         self.descr = Descr(T_HERMITIAN, F_UPPER, D_NON_UNIT)       # IHO:23
+        self.h_descr = self.a_descr = self.descr                    # H mv (IHO:292,314), term7 mv (:551)
+        self.fcoef, self.x_w = omega, None                          # -omega F x ; <x> unweighted (Fock)
         empty = Sparse.csr(np.zeros((n, n)))
         self.empty = empty
         # annihilation: the distance-1 diagonal sqrt(i+1) (mkl_dcsrdia of sqrt_n_append1, IHO:80-94)
@@ -290,12 +330,17 @@ class IhoMkl:
         mkl().cblas_zdotc_sub(self.N, _p(a), 1, _p(b), 1, _p(r))
         return float(r[0].real)
 
+    def _avg(self, a, b) -> float:
+        """temp.real (Fock) or temp.real * grid_size (grid, QO:235,460,482) of zdotc(a, b)"""
+        v = self.zdotc_re(a, b)
+        return v if self.x_w is None else v * self.x_w
+
     def daxpy(self, a: float, x, y):
         mkl().cblas_daxpy(2 * self.N, a, _p(x), 1, _p(y), 1)
 
     def x_expct(self, psi) -> float:
         xs = self.x_state(1.0, psi, 0.0, None)
-        return self.zdotc_re(psi, xs)
+        return self._avg(psi, xs)
 
     def reset_ab(self, dt: float, force: float):
         """IHO:222-277: ab (5 x N, imaginary parts), its LU, and the correction factor A."""
@@ -328,7 +373,7 @@ class IhoMkl:
         xs = self.x_state(1.0, state, 0.0, None).copy()
         rel = xs.copy()
         self.daxpy(-x_avg, state, rel)
-        self.H.mv(complex(0., -1.), self.descr, state, complex(0., self.omega * force), xs)
+        self.H.mv(complex(0., -1.), self.h_descr, state, complex(0., self.fcoef * force), xs)
         result = xs.copy()
         xs = rel.copy()
         self.x_state(1.0, rel, -x_avg, xs)
@@ -338,10 +383,10 @@ class IhoMkl:
     def D1ImRe(self, state, force, gamma):
         """IHO:301-318 -> (resultIm, resultRe, relative_state)"""
         rIm = self.x_state(1.0, state, 0.0, None).copy()
-        x_avg = self.zdotc_re(state, rIm)
+        x_avg = self._avg(state, rIm)
         rel = rIm.copy()
         self.daxpy(-x_avg, state, rel)
-        self.H.mv(complex(0., -1.), self.descr, state, complex(0., self.omega * force), rIm)
+        self.H.mv(complex(0., -1.), self.h_descr, state, complex(0., self.fcoef * force), rIm)
         rRe = rel.copy()
         self.x_state(-gamma / 4., rel, x_avg * gamma / 4., rRe)
         return rIm, rRe, rel
@@ -350,7 +395,7 @@ class IhoMkl:
         """IHO:321-333 (in place on rr)"""
         if not precomputed:
             rr[:] = self.x_state(1.0, state, 0.0, None)
-            x_avg = self.zdotc_re(state, rr)
+            x_avg = self._avg(state, rr)
             self.daxpy(-x_avg, state, rr)
         mkl().cblas_zdscal(self.N, sqrt(gamma / 2.), _p(rr), 1)
 
@@ -388,7 +433,7 @@ class IhoMkl:
         self.D2(Phim, gamma, D2Pm, False)
         # simple_sum_up (IHO:546-573), the loop over the 2N doubles written in the same order
         term7 = np.zeros(n, np.complex128)
-        self.A.mv(complex(1., 0.), self.descr, D1s, complex(0., 0.), term7)
+        self.A.mv(complex(1., 0.), self.a_descr, D1s, complex(0., 0.), term7)
         s = psi.view(np.float64)
         d2, sub, pRe, mRe = D2s.view(np.float64), D1pIm.view(np.float64), D1pRe.view(np.float64), D1mRe.view(np.float64)
         d1, yp, ym = D1s.view(np.float64), D2Yp.view(np.float64), D2Ym.view(np.float64)
@@ -400,11 +445,223 @@ class IhoMkl:
               + 0.25 / dt * (dW * dW / 3 - dt) * dW * (pp - pm - yp + ym)
               - 0.25 * sqrt(dt) * dW * (sub)
               + t7)
-        psi[:] = band_solve(self.ab_LU, self.ipiv, 2, psi)
-        norm = mkl().cblas_dznrm2(n, _p(psi), 1)
-        mkl().cblas_zdscal(n, 1. / norm, _p(psi), 1)
-        fail = int(mkl().cblas_dznrm2(5, _p(psi[n - 5:]), 1) > 2.e-3)   # IHO:422-426
-        return q, x_mean, fail
+        psi[:] = band_solve(self.ab_LU, self.ipiv, self.kl, psi)
+        self.normalize(psi)
+        return q, x_mean, self.fail(psi)
+
+    kl = 2
+
+    def normalize(self, psi):
+        """IHO:216-220"""
+        norm = mkl().cblas_dznrm2(self.N, _p(psi), 1)
+        mkl().cblas_zdscal(self.N, 1. / norm, _p(psi), 1)
+
+    def fail(self, psi) -> int:
+        """check_boundary_error, IHO:422-426"""
+        n = self.N
+        return int(mkl().cblas_dznrm2(5, _p(psi[n - 5:]), 1) > 2.e-3)
+
+
+# --------------------------------------------------------------------------------------- HO stepper
+class HoMkl(IhoMkl):
+    """The harmonic `simulation` module (HO/simulation.cpp) in its own MKL calls. The step is IHO's
+    go_one_step (HO:413-470, simple_sum_up :527-544) with the harmonic Hamiltonian: a diagonal CSR H
+    multiplied under the {DIAGONAL, UPPER} descriptor (HO:23,272,294), term7 under {SYMMETRIC, UPPER}
+    (HO:532), the tridiagonal ab (kl = 1, HO:208-232) and Fail at |psi[N-5:]| > 1e-3 (HO:403-407)."""
+
+    kl = 1
+
+    def __init__(self, n_max: int, omega: float):
+        self.n_max, self.N, self.omega = n_max, n_max + 1, omega
+        n = self.N
+        self.h_descr = Descr(T_DIAGONAL, F_UPPER, D_NON_UNIT)      # HO:23
+        self.a_descr = Descr(T_SYMMETRIC, F_UPPER, D_NON_UNIT)     # HO:252,532
+        self.descr = self.h_descr
+        self.fcoef, self.x_w = omega, None
+        empty = Sparse.csr(np.zeros((n, n)))
+        self.empty = empty
+        ann_d = np.zeros((n, n), np.complex128)                     # mkl_dcsrdia of sqrt_n_append1 (HO:86-97)
+        for i in range(n - 1):
+            ann_d[i, i + 1] = sqrt(float(i + 1))
+        ann = Sparse.csr(ann_d).copy(T_GENERAL, F_UPPER, D_NON_UNIT)
+        cre = ann.add(OP_T, 1.0, empty)                             # HO:98
+        t = cre.add(OP_N, complex(sqrt(0.5), 0.0), empty)           # HO:101-102
+        self.x_hat = ann.add(OP_N, complex(sqrt(0.5), 0.0), t)
+        # H = omega (0.5 + n) on the diagonal (mkl_zcsrdia, HO:119-124)
+        self.H = Sparse.csr(np.diag([omega * (0.5 + float(i)) for i in range(n)]).astype(np.complex128))
+        mkl().mkl_sparse_order(self.H.h)                            # HO:125-131
+        mkl().mkl_sparse_order(self.x_hat.h)
+        self.H.hint_optimize(self.h_descr, 100000000)
+        mkl().mkl_sparse_optimize(self.x_hat.h)
+        sq1 = np.array([sqrt(float(i + 1)) for i in range(n - 1)] + [0.0])
+        self.x_lower = sq1 * sqrt(0.5)                              # x_lower_diag (HO:70-75)
+        self.x_lower_ab = -self.x_lower * 0.5 * omega
+        self.ab_center = np.array([omega * (0.5 + float(i)) * 0.5 for i in range(n)])
+        self._dt = self._force = None
+
+    def reset_ab(self, dt: float, force: float):
+        """HO:208-258: ab (3 x N, imaginary parts: the x coupling on +-1, H dt / 2 on the diagonal), its LU,
+        and the correction factor A (same spmm / z_add chain as the IHO, SYMMETRIC hint)."""
+        n, om = self.N, self.omega
+        ab = np.zeros((3, n), np.complex128)
+        ab[1].real = 1.0
+        ab[2, :n - 1].imag = self.x_lower_ab[:n - 1] * (dt * force)    # dcopy + dscal (HO:213-214)
+        ab[0, 1:].imag = ab[2, :n - 1].imag                           # HO:216
+        ab[1].imag = self.ab_center * dt                              # HO:222-224
+        self.ab_LU, self.ipiv = band_lu(ab, 1)
+        self.A = _a_chain(self.x_hat.add(OP_N, complex(-om * force, 0.0), self.H), dt, self.empty)
+        self.A.hint_optimize(self.a_descr, 80, order=True)
+        self._dt, self._force = dt, force
+
+    def fail(self, psi) -> int:
+        n = self.N
+        return int(mkl().cblas_dznrm2(5, _p(psi[n - 5:]), 1) > 1.e-3)
+
+
+def _a_chain(h0: Sparse, dt: float, empty: Sparse) -> Sparse:
+    """The correction factor dt^3/12 H^2 - i dt^4/24 H^3 - dt^5/80 H^4 + i dt^6/360 H^5 as the reference
+    builds it: spmm powers, then z_add from the lowest order up (IHO:253-272, HO:234-245, QO:414-425)."""
+    h2 = h0.mm(h0)
+    h3 = h2.mm(h0)
+    h4 = h2.mm(h2)
+    h5 = h2.mm(h3)
+    d3, d4, d5, d6 = dt * dt * dt, dt * dt * dt * dt, dt * dt * dt * dt * dt, dt * dt * dt * dt * dt * dt
+    a5 = h2.add(OP_N, complex(d3 / 12., 0.), empty)
+    a6 = h3.add(OP_N, complex(0., -d4 / 24.), a5)
+    a7 = h4.add(OP_N, complex(-d5 / 80., 0.), a6)
+    return h5.add(OP_N, complex(0., d6 / 360.), a7)
+
+
+# ------------------------------------------------------------------------------------- grid stepper
+class GridMkl(IhoMkl):
+    """The quartic `simulation` module (QO/simulation_quart.cpp; the inverted quartic's file is the same
+    code with lambda < 0) in its own MKL calls: Set_World's dense -> CSR operators (QO:46-200), reset_ab
+    (:394-432), D1 / D1ImRe / D2 with the diagonal x and the 9-band H under {SYMMETRIC, UPPER} (:434-486,
+    :25), simple_sum_up (:626-644), zgbtrs with kl = 4 (:622), normalize with sqrt(h) (:259-263), the
+    two-ended check_boundary_error (:559-565) and compute_statistics (:326-362)."""
+
+    kl = 4
+
+    def __init__(self, x_max: float, grid_size: float, lambda_: float, mass: float, moment_order: int = 5):
+        h = grid_size
+        xc = int(x_max / h + 0.5)
+        n = 2 * xc + 1
+        self.N, self.h, self.mass, self.lam, self.moment_order = n, h, mass, lambda_, moment_order
+        self.omega = None
+        self.descr = Descr(T_SYMMETRIC, F_UPPER, D_NON_UNIT)       # QO:25
+        self.h_descr = self.a_descr = self.descr
+        self.herm = Descr(T_HERMITIAN, F_UPPER, D_NON_UNIT)         # p_hat (QO:198,239,285)
+        self.fcoef, self.x_w = pi, h
+        self.x = np.array([h * float(i - xc) for i in range(n)])     # QO:48-50
+        x2 = self.x * self.x
+        V = x2 * x2 * lambda_
+        dx = np.zeros((n, n), np.complex128)                         # QO:59-70
+        for k, v in ((1, 672.), (2, -168.), (3, 32.), (4, -3.)):
+            for i in range(k, n - k):
+                dx[i, i - k] = -v / 840. / h
+                dx[i - k, i] = v / 840. / h
+        d2 = np.zeros((n, n), np.complex128)                         # QO:71-93
+        self.ab_upper = np.zeros((4, n))
+        self.ab_lower = np.zeros((4, n))
+        hh = h * h
+        for i in range(n):
+            d2[i, i] = -14350. / 5040. / hh
+        self.ab_center = (d2.diagonal().real * (-1.) / (2. * mass) + V) * 0.5
+        for k, v in ((1, 8064.), (2, -1008.), (3, 128.), (4, -9.)):
+            for i in range(k, n):
+                d2[i, i - k] = v / 5040. / hh
+                d2[i - k, i] = v / 5040. / hh
+                c = 0.5 * d2[i, i - k].real * (-1.) / (2. * mass)
+                self.ab_upper[4 - k, i] = c
+                self.ab_lower[k - 1, i - k] = c
+        self.empty = empty = Sparse.csr(np.zeros((n, n)))
+        # mkl_zdnscsr / mkl_zcsrdia keep the nonzero entries (zeros left out); then mkl_sparse_copy
+        delta_x = Sparse.csr(dx).copy(T_GENERAL, F_UPPER, D_NON_UNIT)                       # QO:118-126
+        delta_2_x = Sparse.csr(d2).copy(T_SYMMETRIC, F_UPPER, D_NON_UNIT)                   # QO:130-137
+        self.x_hat = Sparse.csr(np.diag(self.x).astype(np.complex128)).copy(T_DIAGONAL, F_UPPER, D_NON_UNIT)
+        V_hat = Sparse.csr(np.diag(V).astype(np.complex128)).copy(T_DIAGONAL, F_UPPER, D_NON_UNIT)
+        self.identity = Sparse.csr(np.eye(n, dtype=np.complex128)).copy(T_HERMITIAN, F_UPPER, D_UNIT)
+        self.p_hat = delta_x.add(OP_N, complex(0., -1.), empty)                              # QO:181-182
+        p_hat_2 = delta_2_x.add(OP_N, complex(-1., 0.), empty)
+        self.H = p_hat_2.add(OP_N, complex(1. / (2. * mass), 0.), V_hat)                     # QO:191-199
+        mkl().mkl_sparse_order(self.H.h)
+        mkl().mkl_sparse_order(self.x_hat.h)
+        mkl().mkl_sparse_order(self.p_hat.h)
+        self.H.hint_optimize(self.descr, 10000000)
+        self.p_hat.hint_optimize(self.herm, 1000000)
+        self._keep = (delta_x, delta_2_x, V_hat, p_hat_2)
+        self._dt = self._force = None
+
+    # compute_x_hat_state (QO:214-229): x diagonal, element by element in the reference's order
+    def x_state(self, alpha: float, psi: np.ndarray, beta: float, result):
+        p = psi.view(np.float64).reshape(-1, 2)
+        xs = self.x[:, None]
+        if beta == 0.0:
+            return np.ascontiguousarray((alpha * p) * xs).view(np.complex128).reshape(-1)
+        out = result.view(np.float64).reshape(-1, 2)
+        out *= beta
+        out += (alpha * p) * xs
+        return result
+
+    def reset_ab(self, dt: float, force: float):
+        """QO:394-432. The diagonal's imaginary part is dcopy + dscal + daxpy in MKL (:397-399); the
+        off-diagonals dt * ab_upper / ab_lower (:402-405)."""
+        n, m = self.N, mkl()
+        ab = np.zeros((9, n), np.complex128)
+        ab[4].real = 1.0
+        abd = ab.view(np.float64)                      # [9][2n]: imaginary parts at odd offsets
+        row = 2 * n
+        m.cblas_dcopy(n, _p(self.ab_center), 1, abd[4:].ctypes.data + 8, 2)
+        m.cblas_dscal(n, dt, abd[4:].ctypes.data + 8, 2)
+        m.cblas_daxpy(n, -dt * force * 0.5 * pi, _p(self.x), 1, abd[4:].ctypes.data + 8, 2)
+        up = np.ascontiguousarray(self.ab_upper.reshape(-1))
+        lo = np.ascontiguousarray(self.ab_lower.reshape(-1))
+        m.cblas_dcopy(4 * n, _p(up), 1, abd.ctypes.data + 8, 2)
+        m.cblas_dscal(4 * n, dt, abd.ctypes.data + 8, 2)
+        m.cblas_dcopy(4 * n, _p(lo), 1, abd[5:].ctypes.data + 8, 2)
+        m.cblas_dscal(4 * n, dt, abd[5:].ctypes.data + 8, 2)
+        assert abd.shape[1] == row
+        self.ab = ab
+        self.ab_LU, self.ipiv = band_lu(ab, 4)
+        self.A = _a_chain(self.x_hat.add(OP_N, complex(-pi * force, 0.), self.H), dt, self.empty)
+        self.A.hint_optimize(self.descr, 80, order=True)
+        self._dt, self._force = dt, force
+
+    def normalize(self, psi):
+        norm = mkl().cblas_dznrm2(self.N, _p(psi), 1)
+        mkl().cblas_zdscal(self.N, 1. / norm / sqrt(self.h), _p(psi), 1)
+
+    def fail(self, psi) -> int:
+        n = self.N
+        return int(mkl().cblas_dznrm2(6, _p(psi[n - 6:]), 1) > 5.e-3 or mkl().cblas_dznrm2(6, _p(psi), 1) > 5.e-3)
+
+    def p_expct(self, psi) -> float:
+        """QO:237-243"""
+        y = np.zeros(self.N, np.complex128)
+        self.p_hat.mv(complex(1., 0.), self.herm, psi, complex(0., 0.), y)
+        return self.zdotc_re(psi, y) * self.h
+
+    def moments(self, psi: np.ndarray) -> np.ndarray:
+        """compute_statistics (QO:326-362): <x>, <p>, then the centred moments of orders 2..m."""
+        psi = np.ascontiguousarray(psi, np.complex128)
+        mo, n, h = self.moment_order, self.N, self.h
+        data = [self.x_expct(psi), self.p_expct(psi)]
+        x_rel = self.x - data[0]
+        p_rel = self.identity.add(OP_N, complex(-data[1], 0.), self.p_hat)
+        p_rel.hint_optimize(self.herm, 5)
+        temp = np.zeros((mo + 1, n), np.complex128)
+        tv = temp.view(np.float64).reshape(mo + 1, n, 2)
+        pv = psi.view(np.float64).reshape(n, 2)
+        tv[0] = pv * x_rel[:, None]
+        p_rel.mv(complex(1., 0.), self.herm, psi, complex(0., 0.), temp[1])
+        for i in range(2, mo + 1):
+            p_rel.mv(complex(1., 0.), self.herm, temp[i - 1], complex(0., 0.), temp[i])
+        for j in range(2, mo + 1):
+            for i in range(j):
+                tv[i] *= x_rel[:, None]
+            for i in range(j + 1):
+                data.append(self.zdotc_re(psi, temp[i]) * h)
+        return np.array(data)
 
 
 # ------------------------------------------------------------------------------- quartic p̂ - p̄ I

@@ -112,11 +112,12 @@ def test_batched_env_iqo_and_cooling_run():
 
 
 def test_wavefunction_input_matches_numpy_on_oracle_state(oracle_mod):
-    """get_data_wavefunction (IHO/main_parallel.py:133-135 state[:-20]; IQO/main_parallel.py:136-137
-    state[10:-10]) * input_scaling in float32, from the device kernel, equals numpy on the oracle's state
+    """get_data_wavefunction (IHO/main_parallel.py:133-135 state[:-20]; HO/main_parallel.py:132-134
+    state[:-10]; IQO/main_parallel.py:136-137 state[10:-10]) * input_scaling in float32, from the device kernel, equals numpy on the oracle's state
     bit for bit; BatchedEnv(input='wavefunction') observes it and stores it in its experience rows."""
     from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper
-    for ph, lo, hi in ((cfg.DEFAULTS[cfg.IHO], 0, -20), (cfg.DEFAULTS[cfg.IQO].with_(x_max=6.4), 10, -10)):
+    for ph, lo, hi in ((cfg.DEFAULTS[cfg.IHO], 0, -20), (cfg.DEFAULTS[cfg.HO], 0, -10),
+                       (cfg.DEFAULTS[cfg.IQO].with_(x_max=6.4), 10, -10)):
         o = oracle_mod.OracleSystem(ph.family, n_max=ph.n_max, x_max=ph.x_max, grid_size=ph.grid_size,
                                     lambda_=ph.lambda_, mass=ph.mass)
         B = 3
@@ -128,7 +129,7 @@ def test_wavefunction_input_matches_numpy_on_oracle_state(oracle_mod):
         st = Stepper(ph, B, 0)
         got = st.wavefunction_obs(torch.from_numpy(ref).cuda(), 0.7).cpu().numpy()
         want = np.hstack((np.real(ref[:, lo:hi]), np.imag(ref[:, lo:hi]))).astype(np.float32) * np.float32(0.7)
-        assert got.shape == (B, 2 * (ph.dim - 20)) and got.dtype == np.float32
+        assert got.shape == (B, 2 * (ph.dim - lo + hi)) and got.dtype == np.float32
         assert np.array_equal(got, want)
     env = BatchedEnv(cfg.DEFAULTS[cfg.IHO], 4, 0, seed=2, input="wavefunction", input_scaling=2.0)
     obs = env.reset()

@@ -84,3 +84,24 @@ def test_env_measurement_mode_loop():
         assert torch.equal(rows[:, L + m], fs)
         assert torch.equal(rows[:, -2], a.float()) and torch.equal(rows[:, -1], r)
         assert torch.equal(obs[live, 1, :m], fs[live, None].expand(-1, m))
+
+
+def test_record_out_of_range_action_is_reported():
+    """qc_record clamps an out-of-range action on the device and raises the handle's error word, so the
+    next check() reports it like a bad qc_step action (no silent clamping)."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=63)
+    B = 4
+    st = Stepper(ph, B, 0, seed=2)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=8)
+    rec = MeasurementRecord(st)
+    ok = torch.full((B,), 10, dtype=torch.int32, device="cuda")
+    out = st.step(psi, ok, ph.control_interval, want_q=True)
+    rec.record(out["q"], ok)
+    st.check()
+    bad = torch.tensor([10, 25, 3, 10], dtype=torch.int32, device="cuda")
+    rec.record(out["q"], bad)
+    with pytest.raises(ValueError, match="actions must lie"):
+        st.check()
+    st.check()      # cleared
+    assert torch.isfinite(rec.hist).all()

@@ -171,3 +171,104 @@ def test_batched_env_shards_equal_single_run_with_auto_reset():
     torch.cuda.synchronize()
     assert n_done > 0
     assert torch.equal(full.psi[:4], halves[0].psi) and torch.equal(full.psi[4:], halves[1].psi)
+
+
+FIX2 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_v2.npz")
+
+
+@pytest.mark.parametrize("name", ["ho71", "ho256", "qo171", "iqo513"])
+def test_dropin_set_seed_reproduces_mkl_reference_trajectory_v2(name):
+    """The harmonic and grid modules through the drop-in with the drivers' call sequence — load(family,
+    ...), set_seed(seed), then step(state, dt, force, gamma) 1000 times, get_moments(state, data) at the
+    snapshots — against the MKL-call-ordered steppers (tests/golden/mklref.py HoMkl / GridMkl, fixtures
+    mkl_v2.npz): psi to 1e-9 (grid norm weighted by sqrt(h)) after 100 / 500 / 1000 steps, every step's q and
+    x_mean to 1e-9, Fail never raised, and compute_statistics' 20 moments to 1e-9 relative."""
+    import json
+    with np.load(FIX2) as z:
+        c = json.loads(bytes(z[f"traj/{name}/params"]).decode())
+        acts, psi0 = z[f"traj/{name}/actions"], z[f"traj/{name}/psi0"]
+        ref_q, ref_x, ref_psi = z[f"traj/{name}/q"], z[f"traj/{name}/x_mean"], z[f"traj/{name}/psi"]
+        ref_m = z[f"traj/{name}/moments"] if c["kind"] == "grid" else None
+    ts = int(round(1 / c["dt"]))
+    if c["kind"] == "ho":
+        sim = S.load(cfg.HO, n_max=c["n_max"], omega=c["omega"], gamma=c["gamma"], time_steps=ts,
+                     f_max=c["f_max"])
+        w = 1.0
+    else:
+        fam = cfg.IQO if c["lam"] < 0 else cfg.QO
+        sim = S.load(fam, x_max=c["x_max"], grid_size=c["h"], lambda_=c["lam"], mass=c["mass"],
+                     gamma=c["gamma"], time_steps=ts, f_max=c["f_max"])
+        w = np.sqrt(c["h"])
+    sim.set_seed(int(c["seed"]))
+    state = psi0.copy()
+    qs, xs, errs, merrs = [], [], [], []
+    snap = 0
+    for k in range(len(ref_q)):
+        F = (int(acts[k // c["ci"]]) - 10) * (c["f_max"] / 10.)
+        q, xm, fail = sim.step(state, c["dt"], F, c["gamma"])
+        assert fail == 0, k
+        qs.append(q)
+        xs.append(xm)
+        if k + 1 in (100, 500, 1000):
+            errs.append(np.linalg.norm(state - ref_psi[snap]) * w)
+            if ref_m is not None:
+                data = np.zeros(20)
+                sim.get_moments(state, data)
+                merrs.append(np.abs(data - ref_m[snap]).max() / max(1.0, np.abs(ref_m[snap]).max()))
+            snap += 1
+    assert np.abs(np.array(qs) - ref_q).max() < 1e-9
+    assert np.abs(np.array(xs) - ref_x).max() < 1e-9
+    assert max(errs) < 1e-9, errs
+    if ref_m is not None:
+        assert max(merrs) < 1e-9, merrs
+    print(f"{name}: |psi - psi_mkl| = {errs[-1]:.2e} after 1000 steps" +
+          (f", moments {max(merrs):.1e}" if merrs else ""))
+
+
+def test_injected_and_mt19937_noise_leave_philox_counters_alone():
+    """qcart.h: an injected noise array (and the MT19937 stream, whose normals reach the step kernel the
+    same way) advances neither stream — the per-env Philox counters stay where they were."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=63)
+    B = 4
+    st = Stepper(ph, B, 0, seed=3)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=8)
+    acts = torch.full((B,), 10, dtype=torch.int32, device="cuda")
+    st.step(psi, acts, 7)
+    assert st.env_counters().tolist() == [7] * B
+    nz = torch.randn((5, B, 2), dtype=torch.float64, device="cuda")
+    st.step(psi, acts, 5, noise=nz)
+    assert st.env_counters().tolist() == [7] * B
+    st.set_seed_mt19937([1, 2, 3, 4])
+    c = st.env_counters()
+    st.step(psi, acts, 6)
+    assert torch.equal(st.env_counters(), c)
+
+
+def test_mt19937_zero_word_matches_mkl(oracle_mod):
+    """Device MT19937 states with planted zero words (mkl_v2.npz zero/*, saved from MKL's own stream):
+    the step kernel consumes MKL's normals for them — finite at u1 = 0 (MKL's radius 3.4244955099270222),
+    0 at u2 = 0 — so the trajectories equal the oracle fed MKL's normals (1e-12) and stay finite."""
+    with np.load(FIX2) as z:
+        states, normals = z["zero/state"], z["zero/normals"]
+    B = len(states)
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=63)
+    st = Stepper(ph, B, 0)
+    st.set_seed_mt19937(list(range(B)))
+    W = 626
+    new = np.zeros((B, W), np.uint32)
+    new[:, :625] = states
+    st.mt19937_state(torch.from_numpy(new.view(np.int32)))
+    psi = st.new_state()
+    psi[:, 0] = 1.0
+    psi0 = psi.cpu().numpy()
+    acts = np.full(B, 13, np.int32)
+    n = normals.shape[1] // 2
+    st.step(psi, torch.from_numpy(acts).cuda(), n)
+    got = psi.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    o = oracle_mod.OracleSystem(1, n_max=63)
+    ref = psi0.copy()
+    o.run_batch(ref, acts, ph.f_max, n, ph.dt, ph.gamma, noise=normals.reshape(B, n, 2).transpose(1, 0, 2).copy(),
+                n_threads=1)
+    assert np.abs(got - ref).max() < 1e-12

@@ -168,3 +168,76 @@ def test_default_mkl_stream_trajectory_deviation_is_bounded(fx):
         b = fx[f"traj/{name}/default/psi"][-1]
         d = np.linalg.norm(a - b)
         assert 0 < d < 1e-5, (name, d)
+
+
+# ---- mkl_v2.npz: the harmonic and grid modules' go_one_step and compute_statistics in MKL call order
+FIX2 = os.path.join(HERE, "golden", "mkl_v2.npz")
+V2_CASES = ["ho71", "ho256", "qo171", "iqo513"]
+
+
+@pytest.fixture(scope="module")
+def fx2():
+    with np.load(FIX2) as z:
+        return {k: z[k] for k in z.files}
+
+
+def v2_system(fx2, name):
+    c = json.loads(bytes(fx2[f"traj/{name}/params"]).decode())
+    if c["kind"] == "ho":
+        return c, O.OracleSystem(O.HO, n_max=c["n_max"], omega=c["omega"])
+    fam = O.IQO if c["lam"] < 0 else O.QO
+    return c, O.OracleSystem(fam, x_max=c["x_max"], grid_size=c["h"], lambda_=c["lam"], mass=c["mass"])
+
+
+@pytest.mark.parametrize("name", V2_CASES)
+def test_oracle_tracks_mkl_ordered_stepper_v2(fx2, name):
+    """mklref.HoMkl / GridMkl (HO/simulation.cpp:413-470,527-554; QO/simulation_quart.cpp:394-432,
+    :434-486, :569-644 with its SYMMETRIC / DIAGONAL descriptors) and the oracle, fed the same MKL noise
+    and actions from the same psi0, agree to 1e-9 in psi (grid: weighted by sqrt(h)) at steps 100 / 500 /
+    1000 and in every step's q and x_mean; Fail is never raised; the oracle's own MT19937 stream of the
+    case's seed reproduces the trajectory; and on the grid the oracle's 20 moments of each MKL snapshot
+    equal compute_statistics' (QO:326-362) to 1e-9 relative. (psi is compared at step 1000; the 100 /
+    500 snapshots fall inside control intervals and are checked by the GPU drop-in test.)"""
+    c, s = v2_system(fx2, name)
+    acts, ci = fx2[f"traj/{name}/actions"], c["ci"]
+    w = np.sqrt(c["h"]) if c["kind"] == "grid" else 1.0
+    for source in ("fixture", "oracle_mt"):
+        if source == "fixture":
+            r = fx2[f"traj/{name}/noise"]
+        else:
+            r = O.MT19937(int(c["seed"])).normals(2 * len(fx2[f"traj/{name}/q"])).reshape(-1, 2)
+        psi = fx2[f"traj/{name}/psi0"].copy().reshape(1, -1)
+        qs, xs, snaps = [], [], []
+        k0 = 0
+        for a in acts:
+            n = min(ci, len(r) - k0)
+            fail, q, xm = s.run_batch(psi, np.array([a], np.int32), c["f_max"], n, c["dt"], c["gamma"],
+                                      noise=r[k0:k0 + n].reshape(n, 1, 2), want_q=True, n_threads=1)
+            assert fail[0] == 0
+            qs.append(q[:, 0])
+            xs.append(xm[:, 0])
+            k0 += n
+        q, xm = np.concatenate(qs), np.concatenate(xs)
+        assert np.abs(q - fx2[f"traj/{name}/q"]).max() < 1e-9, source
+        assert np.abs(xm - fx2[f"traj/{name}/x_mean"]).max() < 1e-9, source
+        err = np.linalg.norm(psi[0] - fx2[f"traj/{name}/psi"][-1]) * w
+        assert err < 1e-9, (source, err)
+    assert not fx2[f"traj/{name}/fail"].any()
+    if c["kind"] == "grid":
+        for snap, ref in zip(fx2[f"traj/{name}/psi"], fx2[f"traj/{name}/moments"]):
+            got = s.moments(snap)
+            assert got.shape == (20,)
+            assert np.abs(got - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max())
+
+
+def test_boxmuller_zero_word_equals_mkl(fx2):
+    """A zero first word (u1 = 0, 2^-32 per normal): MKL's BOXMULLER gives the finite radius
+    3.4244955099270222, not an infinite normal. States with planted zero words (saved / loaded through
+    vslSaveStreamM / vslLoadStreamM, make_mkl_fixtures_v2.py): the oracle's next 8 normals equal MKL's
+    CBWR=COMPATIBLE output to <= 2 ulp, the zero-word ones included (and zero second words give 0)."""
+    for st, ref in zip(fx2["zero/state"], fx2["zero/normals"]):
+        mt = O.MT19937(0)
+        mt.st[:] = st
+        got = mt.normals(len(ref))
+        assert np.all(np.isfinite(got))
+        assert np.all(np.abs(got - ref) <= 2 * np.spacing(np.abs(ref))), (got, ref)

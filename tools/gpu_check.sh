@@ -8,7 +8,7 @@ ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 ok $rc || exit $rc
-timeout -k 10 1200 python -m pytest tests -m gpu -q --timeout 600 "$@" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread "$@" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
 timeout -k 10 600 python bench.py --steps 5 --warmup 1 --cpu-seconds 8 > gpurun_out/bench.log 2>&1; rc=$?

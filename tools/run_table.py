@@ -24,7 +24,7 @@ def main(tag="r01"):
         gbs = hbm / (sm["avg_ms"] * 1e-3) / 1e9 if hbm else None
         row = {"config": c, "N": bl["config"]["seq_len"], "batch": bl["config"]["global_batch"], "dtype": bl["dtype"],
                "env_steps_per_s": bl["value"], "kernel_ms": rf["kernel_ms"], "prof_kernel_ms": sm["avg_ms"],
-               "hbm_frac": rf["frac"], "valu_frac": bl["valu"]["frac"], "rocprof_hbm_gbs": gbs,
+               "hbm_frac": rf["frac"], "valu_frac": (rf["binding"]["frac"] if "binding" in rf else bl["valu"]["frac"]), "rocprof_hbm_gbs": gbs,
                "cpu_env_steps_per_s": cpu.get("value"), "cpu_threads": cpu.get("cores"),
                "cpu_single_core": cpu.get("single_core_value")}
         out.append(row)

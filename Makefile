@@ -3,7 +3,11 @@ HIPCC ?= /opt/rocm/bin/hipcc
 PKG := deepreinforcementlearningcontrolofquantumcartpoles_amd
 CSRC := $(PKG)/csrc
 LIB := $(PKG)/libqcart.so
-HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function
+# -ffp-contract=on: a * b + c is fused where the source writes it as one expression and nowhere else, so
+# every instantiation of a step body (table placements, single- and two-slot workgroups) does bit-identical
+# arithmetic; an env's trajectory never depends on which workgroup shape it ran in (the backend's "fast"
+# contraction fused differently per instantiation)
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -ffp-contract=on
 OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o)
 HDRS := include/qcart.h $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
 
@@ -17,10 +21,10 @@ $(CSRC)/build/qcart_k_grid.o: KFLAGS :=
 # fp32 TU: complex values as packed 2-lane vectors (QCART_F32_PACKED, explicit v_pk_* arithmetic; MS property
 # accessors keep .re/.im) and no SLP packing of the remaining scalar code (it would reshuffle the pairs)
 $(CSRC)/build/qcart_k_f32.o: KFLAGS += -fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED
-$(CSRC)/build/%.o: $(CSRC)/%.hip $(HDRS)
+$(CSRC)/build/%.o: $(CSRC)/%.hip $(HDRS) Makefile
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c $< -o $@
-$(CSRC)/build/%.o: $(CSRC)/%.cpp $(HDRS)
+$(CSRC)/build/%.o: $(CSRC)/%.cpp $(HDRS) Makefile
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

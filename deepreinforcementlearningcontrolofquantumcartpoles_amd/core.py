@@ -159,11 +159,6 @@ class Stepper:
         self.n_slots = max(self.n_slots, slot + 1)
         return slot
 
-    @property
-    def waves_per_env(self) -> int:
-        """1, or 2 for the opt-in two-waves-per-env step kernel (QCART_WE=2 at creation; qc_step_waves_per_env)."""
-        return int(L.lib().qc_step_waves_per_env(self._h))
-
     def scan_levels(self, action: int):
         f, b = ctypes.c_int32(), ctypes.c_int32()
         L.check(L.lib().qc_scan_levels(self._h, action, ctypes.byref(f), ctypes.byref(b)), self._h)

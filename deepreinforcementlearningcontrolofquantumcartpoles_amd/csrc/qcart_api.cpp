@@ -36,7 +36,6 @@ struct qc_handle {
     hipStream_t stream = nullptr;
     int R = 0;
     int wpb = 4;   // envs per step workgroup (step_waves)
-    int we = 1;    // waves per env of the step kernel (2: IHO at large N, rows split over a wave pair)
     bool mirror = false;
     OpHost op;
     std::vector<ActHost> acts;
@@ -58,6 +57,10 @@ struct qc_handle {
     uint32_t slot_bytes = 0;
     int32_t* d_order = nullptr;   // envs grouped by force slot (step kernel with per-block LDS tables)
     size_t order_cap = 0;
+    // two-slot remainder workgroups (k_group order_mixed, k_step DUAL): bytes of one slot's MODE 3 LDS
+    // image, 0 = not used by this handle (QCART_DUAL=0 turns them off, for A/B)
+    uint32_t dual_img = 0;
+    int32_t* d_order_mixed = nullptr;   // [kMaxSlots][wpb]
     int32_t *d_kf = nullptr, *d_kb = nullptr;
     int32_t* d_bad = nullptr;     // raised by k_group on an out-of-range action (qc_take_errors)
 };
@@ -112,6 +115,7 @@ void free_dev(qc_handle* h) {
     if (h->d_bad) { (void)hipFree(h->d_bad); h->d_bad = nullptr; }
     if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
     if (h->d_order) { (void)hipFree(h->d_order); h->d_order = nullptr; h->order_cap = 0; }
+    if (h->d_order_mixed) { (void)hipFree(h->d_order_mixed); h->d_order_mixed = nullptr; }
     if (h->d_kb) { (void)hipFree(h->d_kb); h->d_kb = nullptr; }
     if (h->d_ctr) { (void)hipFree(h->d_ctr); h->d_ctr = nullptr; }
     if (h->d_mt) { (void)hipFree(h->d_mt); h->d_mt = nullptr; }
@@ -135,7 +139,7 @@ int upload(qc_handle* h, T** dst, const T* src, size_t n) {
 int upload_tables(qc_handle* h) {
     const int Np = h->op.Npad, kl = h->op.kl, R = h->op.Rs, LN = h->op.lanes;
     const bool f32 = h->p.precision == QC_FP32;   // fp32 blocks: the fp64 factors rounded once
-    const bool sym = !h->op.fock || LN > kWave;   // L D L^T, no uc band (SlotLayout)
+    const bool sym = h->op.sym;   // L D L^T, no uc band (SlotLayout, slot_sym)
     const SlotLayout L = slot_layout(kl, R, h->op.family == QC_IHO, f32 ? 8u : 16u, sym, LN);
     h->slot_bytes = L.bytes;
     std::vector<uint8_t> tab((size_t)kMaxSlots * L.bytes, 0);
@@ -227,26 +231,26 @@ KArgs base_args(const qc_handle* h) {
         }
         const bool f32 = p.precision == QC_FP32;
         const uint32_t es = f32 ? 8u : 16u;   // bytes per complex table element
-        const bool pair = h->we == 2;
-        const SlotLayout L = slot_layout(op.kl, op.Rs, op.family == QC_IHO, es, !op.fock || pair, op.lanes);
+        const SlotLayout L = slot_layout(op.kl, op.Rs, op.family == QC_IHO, es, op.sym, op.lanes);
         // MODE 2 image: levels 0..NL-1 + the row prefix per direction at fixed places (needs kf, kb <= NL)
         const int NL = mode2_levels(op.kl);
         const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * op.lanes * es;
         // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane), the grid its
         // row constants (H_F's folded diagonal and x_r: 2R doubles per lane, RowLds)
-        // (the pair kernel reads no force coefficients from LDS; its mailboxes precede the image)
-        const size_t fx = pair ? 0
-                          : op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
-                                    : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
-        const size_t mb = pair ? (size_t)8 * kPairMailbox : 0;
-        int mode = (mb + t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (mb + t1 + fx <= 160 * 1024 ? 1 : 0);
+        const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
+                                  : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
+        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
         a.tab_mode = mode;
         a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);
-        a.lds_bytes = mode ? (uint32_t)(mb + a.lds_fx + fx) : (uint32_t)mb;
+        a.lds_bytes = mode ? (uint32_t)(a.lds_fx + fx) : 0u;
+        // two-slot blocks (MODE 3) share the launch: the dynamic LDS covers two slot images
+        if (h->dual_img && mode >= 1) {
+            a.lds_img = h->dual_img;
+            a.lds_bytes = std::max(a.lds_bytes, 2u * h->dual_img);
+        }
     }
     a.precision = p.precision;
-    a.we = h->we;
     a.order = nullptr;
     a.n_blocks = (uint32_t)((p.batch + h->wpb - 1) / h->wpb);
     a.n_obs = qc_n_obs(h);
@@ -351,13 +355,7 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
         delete h;
         return QC_ENOTBUILT;
     }
-    // IHO at large N (R = 16 fp64 / 32 fp32 in one wave: one wave per SIMD, spilling): QCART_WE=2 splits
-    // each env over a wave pair at R / 2 rows per lane. Opt-in: measured slower than one wave per env
-    // (C5: 94 vs 51.6 ms per launch; DESIGN.md §4 "two waves per env")
-    const char* we_env = std::getenv("QCART_WE");
-    const bool want_pair = we_env && std::atoi(we_env) == 2 && p->family == QC_IHO && (h->R % 2 == 0) &&
-                           step_waves(p->family, h->R / 2, p->precision, 2) > 0;
-    h->wpb = want_pair ? step_waves(p->family, h->R / 2, p->precision, 2) : step_waves(p->family, h->R, p->precision);
+    h->wpb = step_waves(p->family, h->R, p->precision);
     if (h->wpb <= 0) {
         set_create_err("no step kernel for N = " + std::to_string(probe.N));
         delete h;
@@ -365,26 +363,10 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     }
     rc = build_ops(p->family, p->n_max, p->omega, p->x_max, p->grid_size, p->lambda_, p->mass, h->R, h->op, err);
     if (rc) { set_create_err(err); delete h; return rc; }
-    if (want_pair) {
-        h->we = 2;
-        h->op.lanes = 2 * kWave;
-        h->op.Rs = h->R / 2;
-    }
+    const uint32_t es = p->precision == QC_FP32 ? 8u : 16u;
+    h->op.sym = slot_sym(h->op.fock, es, h->op.lanes);
     rc = build_all_actions(h);
     if (rc) { set_create_err(h->err); delete h; return rc; }
-    if (h->we == 2) {
-        // the pair kernel's scan is the two-level one (<= 4 in-row levels per direction)
-        bool ok = true;
-        for (auto& s : h->acts) ok = ok && s.kf <= 4 && s.kb <= 4;
-        if (!ok) {
-            h->we = 1;
-            h->op.lanes = kWave;
-            h->op.Rs = h->R;
-            h->wpb = step_waves(p->family, h->R, p->precision);
-            rc = build_all_actions(h);
-            if (rc) { set_create_err(h->err); delete h; return rc; }
-        }
-    }
     DeviceGuard g(device);
     const int Np = h->op.Npad;
     if ((rc = upload(h, &h->d_xu, h->op.xu.data(), Np)) || (rc = upload(h, &h->d_xg, h->op.xg.data(), Np)) ||
@@ -393,6 +375,10 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
         free_dev(h);
         delete h;
         return rc;
+    }
+    {
+        const char* de = std::getenv("QCART_DUAL");
+        if (!(de && std::atoi(de) == 0)) h->dual_img = (uint32_t)std::max(0, step_dual_img(p->family, h->R, p->precision));
     }
     {
         std::vector<uint64_t> zero((size_t)std::max<int64_t>(p->batch, 1), 0);
@@ -596,11 +582,19 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
             h->order_cap = cap;
         }
+        // two-slot remainder workgroups when the step kernel has them (tables in LDS, fp64, one wave per env)
+        const bool dual = a.lds_img > 0;
+        if (dual && !h->d_order_mixed) {
+            hipError_t e = hipMalloc((void**)&h->d_order_mixed, (size_t)kMaxSlots * W * sizeof(int32_t));
+            if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
         if (launch_group(actions, default_action, env_steps, n_steps, h->p.batch, (int)h->acts.size(), (int)W,
-                         h->d_order, (int32_t)cap, h->d_bad, h->stream))
+                         h->d_order, (int32_t)cap, h->d_bad, dual ? h->d_order_mixed : nullptr, h->stream))
             return fail(h, QC_EHIP, "group kernel launch failed");
         a.order = h->d_order;
         a.n_blocks = (uint32_t)(cap / W);
+        a.order_mixed = dual ? h->d_order_mixed : nullptr;
+        a.n_mixed = dual ? (uint32_t)h->acts.size() : 0u;
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (h->timing) {
@@ -813,8 +807,6 @@ int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, flo
                                  h->stream);
     return rc ? fail(h, QC_EHIP, "wavefunction kernel launch failed") : QC_OK;
 }
-
-int qc_step_waves_per_env(const qc_handle* h) { return h ? h->we : QC_EINVAL; }
 
 int qc_take_errors(qc_handle* h) {
     if (!h) return QC_EINVAL;

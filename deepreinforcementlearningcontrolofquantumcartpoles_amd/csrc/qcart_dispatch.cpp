@@ -45,12 +45,18 @@ bool have_kernel(int family, int R, int precision) {
     return false;
 }
 
-int step_waves(int family, int R, int precision, int we) {
+int step_waves(int family, int R, int precision) {
     KArgs a{};
     a.B = 1;
     a.precision = precision;
-    a.we = we;
     return route(family, R, 4, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr);
+}
+
+int step_dual_img(int family, int R, int precision) {
+    KArgs a{};
+    a.B = 1;
+    a.precision = precision;
+    return route(family, R, 6, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr);
 }
 
 int launch_step(int family, int R, const KArgs& a, void* stream) {

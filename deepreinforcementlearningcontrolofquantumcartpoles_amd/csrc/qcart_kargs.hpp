@@ -14,14 +14,14 @@ namespace qcart {
 //   m2   real    [10][R][64]    2 Im A[r-d][r] (IHO only; zero unless the reference mirror mode)
 //   tf   complex [7][kl*kl][64] forward Kogge-Stone composites, level 6 = in-row prefix product
 //   tb   complex [7][kl*kl][64] backward composites, level 6 = in-row suffix product
-// sym (grid families): ab = I + i dt/2 H_F is complex symmetric, so its pivot-free LU is L D L^T and
+// sym (slot_sym): ab = I + i dt/2 H_F is complex symmetric, so its pivot-free LU is L D L^T and
 // U[r][r+k] / U[r][r] = L[r+k][r]: the backward substitution reads the lc band at row r + k (the next
 // lane's run for rows past the lane) and the block carries no uc band.
 struct SlotLayout {
     uint32_t lc, uc, di, m2, tf, tb, bytes;
 };
 // es: bytes of one complex element (16 fp64, 8 fp32); real bands use es / 2
-// lanes: lanes per env (64; 128 for the two-waves-per-env step kernel) — the run length of every band
+// lanes: lanes per env (64) — the run length of every band
 constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, bool sym = false, int lanes = 64) {
     SlotLayout L{};
     const uint32_t ln = (uint32_t)lanes;
@@ -35,11 +35,14 @@ constexpr SlotLayout slot_layout(int kl, int R, bool has_m2, uint32_t es = 16, b
     return L;
 }
 
+// L D L^T tables (no uc band): every fp64 family (ab = I + i dt/2 H_F is complex symmetric for every
+// Hamiltonian here); the fp32 kernel (C5) keeps the uc band (its L D L^T layout was measured slower:
+// DESIGN.md §4). lanes: the run length of the tables (64 = one wave per env)
+constexpr bool slot_sym(bool fock, uint32_t es, int lanes) { return !fock || lanes > 64 || es == 16; }
+
 // scan levels per direction the MODE 2 LDS image keeps (forward levels, prefix, backward levels, suffix):
 // 4 for the Fock bands (kl <= 2), 2 for the grid's kl = 4 (its 16-element composites)
 constexpr int mode2_levels(int kl) { return kl >= 4 ? 2 : 4; }
-// two-waves-per-env step kernel: LDS mailbox bytes per wave (qcart_kernels.hpp kPairBytes)
-constexpr unsigned kPairMailbox = 1024;
 // grid step kernels that read their per-row constants (H_F's folded diagonal, x_r) from the LDS image
 // instead of holding them in registers: the R = 17 kernel, whose step spills (for R <= 9 the registers
 // are there and the LDS reads cost more than they save: C4 12.6 -> 14.9 ms, C3 29.4 -> 27.9 ms)
@@ -75,7 +78,10 @@ struct KArgs {
     uint32_t lds_bytes;        // dynamic LDS per block for tab_mode >= 1
     uint32_t lds_fx;           // LDS offset of the H_F force coefficients (Fock, tab_mode >= 1)
     const int32_t* order;      // [n_blocks*W] envs grouped by force slot (-1 idle) or null (identity)
-    uint32_t n_blocks;         // step kernel grid
+    uint32_t n_blocks;         // step kernel grid (single-slot workgroups)
+    const int32_t* order_mixed;   // [n_mixed*W] k_group's two-slot remainder workgroups (-1 idle)
+    uint32_t n_mixed;          // two-slot blocks ahead of the n_blocks (0: none; launch_step DUAL)
+    uint32_t lds_img;          // bytes of one slot's MODE 3 image (tables + H_F force coefficients)
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
     double a2, a3, a4, a5;     // Horner coefficients dt^3/12, dt^4/24, dt^5/80, dt^6/360
@@ -102,7 +108,6 @@ struct KArgs {
     // prefactors 0.5/sqrt(dt), 0.25/sqrt(dt), 0.5/dt, 0.25/dt, 0.25 dt, 0.25 sqrt(dt), sqrt(dt) dt 0.5,
     // sqrt(dt) beta and the Horner ratios a2/a5, a3/a5, a4/a5 — each the same fp64 expression as before
     double inv_sdt, inv_dt, k_hisdt, k_qisdt, k_hidt, k_qidt, k_qdt, k_qsdt, k_dz, k_sb, b2, b3, b4;
-    int32_t we;                // waves per env of the step kernel (1, or 2: Fock families at large N)
 };
 
 // measurement-record update (qcart_record.hip, qc_record)
@@ -145,9 +150,12 @@ int launch_reset(int family, int R, const KArgs& a, int kind, const uint8_t* mas
                  void* stream);
 int launch_control(int family, int R, const KArgs& a, void* stream);   // qc_control (act_out / force_out)
 bool have_kernel(int family, int R, int precision = 0);
-int step_waves(int family, int R, int precision = 0, int we = 1);   // envs per step-kernel workgroup (<0: none)
+int step_waves(int family, int R, int precision = 0);   // envs per step-kernel workgroup (<0: none)
+int step_dual_img(int family, int R, int precision = 0);   // MODE 3 slot-image bytes (0: no two-slot blocks)
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
+// order_mixed (optional, [n_slots * gran]): slots with >= gran envs are laid out back to back and cut into
+// gran-env workgroups; the ones that straddle two slots go to order_mixed (k_step DUAL), the rest to order
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
-                 int n_slots, int gran, int32_t* order, int32_t cap, int32_t* bad, void* stream);
+                 int n_slots, int gran, int32_t* order, int32_t cap, int32_t* bad, int32_t* order_mixed, void* stream);
 
 }  // namespace qcart

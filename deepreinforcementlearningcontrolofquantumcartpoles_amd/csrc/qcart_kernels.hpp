@@ -269,65 +269,11 @@ __device__ __forceinline__ void step_sum(double (&v)[NV]) {
     wave_sum<NV>(v);
 }
 
-// ---- two waves per env (k_step WE = 2, Fock families at N > 64 R): an env's rows are split over an
-// adjacent wave pair of the workgroup, half h owning rows [64 R h, 64 R (h + 1)); the pair exchanges
-// boundary rows (stencil halos), partial sums and scan carries through a mailbox per wave at the start of
-// the dynamic LDS. Every exchange is symmetric: both waves write their part, publish the exchange's
-// sequence number and wait for the partner's — no workgroup barrier, so pairs with different step counts
-// never wait on each other. Data is double-buffered by sequence parity: a wave rewrites a buffer two
-// exchanges later, after the partner's publish of the exchange in between proved it done reading it.
-constexpr uint32_t kPairBytes = kPairMailbox;   // per wave: [0] published sequence, [16, 16 + 2 kPairData) data
-constexpr uint32_t kPairData = 448;   // two buffers, then 64 B of scratch words for non-sending lanes
-struct PLane {
-    int l;                 // lane in the wave
-    int half;              // which half of the env's rows this wave owns
-    char* me;              // this wave's mailbox
-    const char* pa;        // the partner's
-    mutable uint32_t seq;  // exchanges so far (the same count in both waves of the pair)
-    __device__ __forceinline__ operator int() const { return l; }
-};
-template <typename LT>
-inline constexpr bool kPair = false;
-template <>
-inline constexpr bool kPair<PLane> = true;
-// this wave's buffer of the next exchange
-__device__ __forceinline__ char* pl_out(const PLane& p) {
-    ++p.seq;
-    return p.me + 16 + (p.seq & 1u) * kPairData;
-}
-// publish, then wait for the partner's part of the same exchange and return its buffer
-// (no divergent branches in the exchanges: every lane stores — the same value, or to a scratch word of the
-// mailbox — and every lane loads and selects, so the step body stays one basic block between the waits)
-__device__ __forceinline__ const char* pl_swap(const PLane& p) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store((uint32_t*)p.me, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    // (back-off between polls: s_sleep 1 measured 94 ms per C5 launch, a tight poll 108 ms)
-    while (__hip_atomic_load((const uint32_t*)p.pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < p.seq)
-        __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return p.pa + 16 + (p.seq & 1u) * kPairData;
-}
-// wave-uniform values summed over the pair (a + b == b + a: both halves get the same bits)
-template <int NV>
-__device__ __forceinline__ void pl_sum(const PLane& p, double (&v)[NV]) {
-    double* o = (double*)pl_out(p);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) o[i] = v[i];   // uniform value, every lane
-    const double* in = (const double*)pl_swap(p);
-    // (the partner's sums are wave-uniform: read into SGPRs, so everything derived stays scalar)
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const unsigned long long u = (unsigned long long)__double_as_longlong(in[i]);
-        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
-        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
-        v[i] = v[i] + mk_d(lo, hi);
-    }
-}
-// the step kernel's reductions over the env (one wave, or the pair)
+// the step kernel's reductions over the env's wave (the lane argument is unused: the call sites pass the
+// stencils' lane context)
 template <int NV, typename LT>
-__device__ __forceinline__ void step_sum(double (&v)[NV], const LT& lane) {
+__device__ __forceinline__ void step_sum(double (&v)[NV], const LT&) {
     wave_sum<NV>(v);
-    if constexpr (kPair<LT>) pl_sum<NV>(lane, v);
 }
 
 // ---- family traits: 0 = HO (Fock, H diagonal), 1 = IHO (Fock, H on +-2), 2 = grid (9-band)
@@ -339,46 +285,6 @@ template <>
 struct Fam<1> { static constexpr int KL = 2; };
 template <>
 struct Fam<2> { static constexpr int KL = 4; };
-
-// pair halos (WE = 2): half 0 sends its last H rows (the partner's lower halo), half 1 its first H rows (the
-// partner's upper halo); the lanes whose halo crosses the wave edge (half 1: rows base-H+t < 0; half 0:
-// rows base+R+t >= 64 R, zero from the in-wave DPP shifts) take them from the partner's buffer.
-// e: [H lower][R own][H upper] (UP) or [H lower] (make_lo: lower halo only).
-template <int R, int H, bool UP, typename RT, int NE>
-__device__ __forceinline__ void pl_halo(const PLane& p, const cx<RT> (&v)[R], cx<RT> (&e)[NE]) {
-    static_assert(2 * H * sizeof(RT) <= kPairData, "halo too wide for the pair mailbox");
-    RT* o = (RT*)pl_out(p);
-    RT* const sink = (RT*)(p.me + 16 + 2 * kPairData);   // scratch words of the mailbox (not read)
-    const int base = p.l * R;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const int g = base + j;   // row in this half
-        const int i = p.half == 0 ? g - (64 * R - H) : g;   // mailbox row: half 0 its last H, half 1 its first H
-        const bool snd = i >= 0 && i < H && (p.half == 0 || UP);
-        RT* d = snd ? o + 2 * i : sink;
-        d[0] = v[j].re;
-        d[1] = v[j].im;
-    }
-    const RT* in = (const RT*)pl_swap(p);
-#pragma unroll
-    for (int t = 0; t < H; ++t) {
-        const int i = base + t;   // half 1, lower halo row base - H + t of half 0's last H rows
-        const bool rcv = p.half == 1 && i < H;
-        const int ic = rcv ? i : 0;
-        const cx<RT> x = C(in[2 * ic], in[2 * ic + 1]);
-        e[t] = C(rcv ? x.re : e[t].re, rcv ? x.im : e[t].im);
-    }
-    if constexpr (UP) {
-#pragma unroll
-        for (int t = 0; t < H; ++t) {
-            const int i = base + R + t - 64 * R;   // half 0, upper halo row base + R + t of half 1's first H rows
-            const bool rcv = p.half == 0 && i >= 0;
-            const int ic = rcv ? i : 0;
-            const cx<RT> x = C(in[2 * ic], in[2 * ic + 1]);
-            e[H + R + t] = C(rcv ? x.re : e[H + R + t].re, rcv ? x.im : e[H + R + t].im);
-        }
-    }
-}
 
 // ---- halos: e[H + j] = v[j]; e[t] = row base-H+t (lanes below), e[H+R+t] = row base+R+t.
 // Lanes outside the wave read 0 (the operators have zero rows there). dl is compile-time: the shift
@@ -407,7 +313,6 @@ __device__ __forceinline__ void make_ext(const cx<RT> (&v)[R], cx<RT> (&e)[R + 2
         else if (dl == 3) e[H + R + t] = C(shl<3>(v[idx].re), shl<3>(v[idx].im));
         else e[H + R + t] = C(shl<4>(v[idx].re), shl<4>(v[idx].im));
     }
-    if constexpr (kPair<LT>) pl_halo<R, H, true>(lane, v, e);
 }
 // lower halo only: e[t] = row base - H + t, t < H (up to 10 rows: dl <= 10 lanes for R = 1)
 template <int R, int H, typename RT, typename LT>
@@ -428,7 +333,6 @@ __device__ __forceinline__ void make_lo(const cx<RT> (&v)[R], cx<RT> (&e)[H], co
             e[t] = C(ok ? re : RT(0), ok ? im : RT(0));
         }
     }
-    if constexpr (kPair<LT>) pl_halo<R, H, false>(lane, v, e);
 }
 
 // ---- per-lane operator coefficients (action independent), loaded once per call
@@ -808,7 +712,7 @@ __device__ __forceinline__ cx<RT> row_shift(cx<RT> v) {
 // below kScanTol (nlev <= 4); otherwise band_solve runs the full 6-level Kogge-Stone with shuffles.
 template <int KL, bool FWD, int MODE, int LE, typename RT>
 __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& tb, uint32_t lv0, uint32_t lvp,
-                                          int nlev, cx<RT> (&pre)[KL]) {
+                                          int nlev) {
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
     // composites are read level by level (KL = 4: 16 complex per level; all levels at once would
     // not fit the register file), fenced for KL = 4 so the next level's reads are not hoisted
@@ -833,8 +737,6 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
             if constexpr (KL > 2) __builtin_amdgcn_sched_barrier(0);
         }
     }
-#pragma unroll
-    for (int k = 0; k < KL; ++k) pre[k] = s[k];   // in-row state (the pair's cross-wave carry)
     cx<RT> P[KL * KL];
 #pragma unroll
     for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * CE);
@@ -881,8 +783,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
             return t.c(SL.uc + (uint32_t)(k * R + j) * CE);
         }
     };
-    const bool hf = MODE == 2 || kf <= 4 || kPair<LT>, hb = MODE == 2 || kb <= 4 || kPair<LT>;
-    cx<RT> pre[KL];
+    const bool hf = MODE == 2 || kf <= 4, hb = MODE == 2 || kb <= 4;
     // forward, pass 1 (zero incoming state): lane end state e_l
     cx<RT> s[KL];
 #pragma unroll
@@ -899,7 +800,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(10);
     if (hf) {
-        scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf, pre);
+        scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf);
     } else {
         // Kogge-Stone over lanes: E_l += T_lvl(l) E_{l - 2^lvl}
         for (int lvl = 0; lvl < kf; ++lvl) {
@@ -924,39 +825,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     Tab<MODE, RT> tb2 = tb;
     if constexpr (KL == 4) asm volatile("" : "+v"(tb2.vc), "+v"(tb2.hc));
     // incoming state from lane - 1, pass 2
-    cx<RT> fin[KL];
-    if constexpr (kPair<LT>) {
-        // half 1's first 16-lane row takes its carry from half 0's lane 63 (in-row state) through the row
-        // prefix product, and its lane 0 the pass-2 incoming state (half 0's lane 63 final state)
-        RT* o = (RT*)pl_out(lane);
-        {
-            RT* d = (lane.half == 0 && lane.l == 63) ? o : (RT*)(lane.me + 16 + 2 * kPairData);
-#pragma unroll
-            for (int k = 0; k < KL; ++k) {
-                d[4 * k] = pre[k].re, d[4 * k + 1] = pre[k].im;
-                d[4 * k + 2] = s[k].re, d[4 * k + 3] = s[k].im;
-            }
-        }
-        const RT* in = (const RT*)pl_swap(lane);
-        {
-            const bool m = lane.half == 1 && lane.l < 16;   // carry only into half 1's row 0 (a select: the
-                                                            // other lanes read the partner's stale buffer)
-#pragma unroll
-            for (int i = 0; i < KL; ++i)
-#pragma unroll
-                for (int k = 0; k < KL; ++k)
-                    s[i] = cmac(s[i], tb.comp(fP + (uint32_t)(i * KL + k) * CE), C(m ? in[4 * k] : RT(0), m ? in[4 * k + 1] : RT(0)));
-        }
-#pragma unroll
-        for (int k = 0; k < KL; ++k) fin[k] = C(in[4 * k + 2], in[4 * k + 3]);
-    }
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
-    if constexpr (kPair<LT>) {
-        const bool r = lane.half == 1 && lane.l == 0;
-#pragma unroll
-        for (int k = 0; k < KL; ++k) s[k] = C(r ? fin[k].re : s[k].re, r ? fin[k].im : s[k].im);
-    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         cx<RT> y = b[j];
@@ -984,7 +854,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     }
     QC_STAMP(13);
     if (hb) {
-        scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb, pre);
+        scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb);
     } else {
         for (int lvl = 0; lvl < kb; ++lvl) {
             const int d = 1 << lvl;
@@ -1005,37 +875,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     QC_STAMP(14);
     Tab<MODE, RT> tb3 = tb;
     if constexpr (KL == 4) asm volatile("" : "+v"(tb3.vc), "+v"(tb3.hc));
-    if constexpr (kPair<LT>) {
-        // half 0's last 16-lane row takes its carry from half 1's lane 0 (in-row state) through the row
-        // suffix product, and its lane 63 the pass-2 incoming state (half 1's lane 0 final state)
-        RT* o = (RT*)pl_out(lane);
-        {
-            RT* d = (lane.half == 1 && lane.l == 0) ? o : (RT*)(lane.me + 16 + 2 * kPairData);
-#pragma unroll
-            for (int k = 0; k < KL; ++k) {
-                d[4 * k] = pre[k].re, d[4 * k + 1] = pre[k].im;
-                d[4 * k + 2] = s[k].re, d[4 * k + 3] = s[k].im;
-            }
-        }
-        const RT* in = (const RT*)pl_swap(lane);
-        {
-            const bool m = lane.half == 0 && lane.l >= 48;   // carry only into half 0's row 3
-#pragma unroll
-            for (int i = 0; i < KL; ++i)
-#pragma unroll
-                for (int k = 0; k < KL; ++k)
-                    s[i] = cmac(s[i], tb.comp(bP + (uint32_t)(i * KL + k) * CE), C(m ? in[4 * k] : RT(0), m ? in[4 * k + 1] : RT(0)));
-        }
-#pragma unroll
-        for (int k = 0; k < KL; ++k) fin[k] = C(in[4 * k + 2], in[4 * k + 3]);
-    }
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
-    if constexpr (kPair<LT>) {
-        const bool r = lane.half == 0 && lane.l == 63;
-#pragma unroll
-        for (int k = 0; k < KL; ++k) s[k] = C(r ? fin[k].re : s[k].re, r ? fin[k].im : s[k].im);
-    }
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {
         cx<RT> x = b[j];
@@ -1171,64 +1012,81 @@ template <int FAM, int R, typename RT = double>
 constexpr int kStepWaves =
     ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= QCART_W8_MAX_RG)) ? 8 : 4;
 
-// waves per step workgroup: WE = 2 (two waves per env) runs 4 env pairs, two waves per SIMD
-template <int FAM, int R, typename RT, int WE>
-constexpr int kBlockWaves = WE == 2 ? 8 : kStepWaves<FAM, R, RT>;
 
-template <int FAM, int R, int MODE, typename RT = double, int WE = 1>
-__global__ __launch_bounds__((64 * kBlockWaves<FAM, R, RT, WE>))
-__attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWaves<FAM, R, RT, WE> / 4)))) void k_step(
-    const KArgs a) {
-    static_assert(WE == 1 || FAM == 1, "two waves per env: IHO only");
+// MODE 3: a two-slot block (k_group's remainder workgroups, KArgs::order_mixed): MODE 1 reads (tables in
+// LDS, scan composites from the slot's global block) with both slots' images in LDS, a.lds_img bytes apart;
+// every wave uses its own env's slot and image
+template <int FAM, int R, int MODE, typename RT>
+__device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, const uint32_t blk) {
     constexpr int KL = Fam<FAM>::KL;
-    constexpr int W = kBlockWaves<FAM, R, RT, WE>;   // waves per block
-    constexpr int EPB = W / WE;                       // envs per block
-    constexpr int LE = 64 * WE;                       // lanes per env
-    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), FAM == 2 || WE == 2, LE);
+    constexpr int W = kStepWaves<FAM, R, RT>;   // waves per block
+    constexpr int EPB = W;                      // envs per block (one wave per env)
+    constexpr int LE = 64;                      // lanes per env
+    constexpr bool SYMT = slot_sym(FAM != 2, (uint32_t)sizeof(cx<RT>), LE);   // L D L^T tables (no uc band)
+    constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), SYMT, LE);
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>), CR = (uint32_t)LE * sizeof(RT);   // lane-run bytes
     const int lane = threadIdx.x & 63;
-    const int half = WE == 2 ? __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1u)) : 0;   // rows owned
-    const int gl = half * 64 + lane;                                   // lane of the env
-    // env of this wave: a.order (envs grouped by force slot, EPB per block, -1 = idle) or identity
-    const int64_t e0 = a.order ? (int64_t)a.order[blockIdx.x * EPB] : (int64_t)blockIdx.x * EPB;
+    const int gl = lane;   // lane of the env
+    // env of this wave: order (envs grouped by force slot, EPB per block, -1 = idle) or identity
+    const int64_t e0 = order ? (int64_t)order[blk * EPB] : (int64_t)blk * EPB;
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
     // (wave-uniform: made explicit, so every env-derived address lives in SGPRs)
-    const int ei = (int)(threadIdx.x >> 6) / WE;
+    const int ei = (int)(threadIdx.x >> 6);
     const int64_t env = (int64_t)__builtin_amdgcn_readfirstlane(
-        a.order ? a.order[blockIdx.x * EPB + ei] : (int)(blockIdx.x * EPB + ei));
+        order ? order[blk * EPB + ei] : (int)(blk * EPB + ei));
     const bool active = env >= 0 && env < a.B;
-    // force slot: per wave (MODE 0), per block (MODE >= 1: the host groups envs so that every wave of a
-    // block shares its first env's slot)
-    int slot = a.actions ? a.actions[(MODE >= 1 || !active) ? e0 : env] : a.default_action;
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    slot = slot < 0 ? 0 : (slot >= a.n_slots ? a.n_slots - 1 : slot);   // never index out of the tables
+    auto clamp_slot = [&](int s) { return s < 0 ? 0 : (s >= a.n_slots ? a.n_slots - 1 : s); };
+    // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
+    // a block shares its first env's slot)
+    const bool per_wave = MODE == 0 || MODE == 3;
+    int slot = a.actions ? a.actions[(!per_wave || !active) ? e0 : env] : a.default_action;
+    slot = clamp_slot(__builtin_amdgcn_readfirstlane(slot));   // never index out of the tables
+    // MODE 3: the block's two slots (its first env's and its last env's) and this wave's image
+    int slotA = slot, slotB = slot;
+    uint32_t img_off = 0;
+    if constexpr (MODE == 3) {
+        int eb = (int)e0;
+#pragma unroll
+        for (int i = 1; i < EPB; ++i) {
+            const int ei2 = order[blk * EPB + i];
+            eb = ei2 >= 0 ? ei2 : eb;
+        }
+        slotA = clamp_slot(__builtin_amdgcn_readfirstlane(a.actions[e0]));
+        slotB = clamp_slot(__builtin_amdgcn_readfirstlane(a.actions[eb]));
+        img_off = slot == slotA ? 0u : a.lds_img;
+    }
     const rsrc_t rs = make_rsrc((const char*)a.tab + (size_t)slot * a.slot_bytes, SL.bytes);
+    // LDS offset of the slot's H_F force coefficients: after the tables in a MODE 3 slot image
+    const uint32_t lds_fx = MODE == 3 ? SL.tf : a.lds_fx;
     const int kf = a.kf[slot], kb = a.kb[slot];
     const double cFd = a.c * a.force[slot];
     const RT cF = (RT)cFd;
     // H_F force coefficients from LDS (apply_hf_fx): fp64 Fock families with the tables in LDS
-    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8 && WE == 1;
+    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8;
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
-    // WE = 2: the pair mailboxes (kPairBytes per wave) precede the table image
-    char* const simg = (char*)smem_dyn + (WE == 2 ? W * kPairBytes : 0u);
-    if constexpr (WE == 2) {
-        if (lane == 0) *(uint32_t*)((char*)smem_dyn + (threadIdx.x >> 6) * kPairBytes) = 0u;
-    }
+    char* const simg0 = (char*)smem_dyn;
+    char* const simg = simg0 + img_off;   // this wave's slot image (MODE 3: slot A's or slot B's)
     // a block of the no-budget group (k_group puts envs with env_steps <= 0 in whole blocks of their
     // own) takes no step: it skips the table image
-    const bool block_idle = a.order && a.env_steps && (a.env_steps[e0] <= 0 || a.n_steps <= 0);
-    if ((MODE >= 1 && !block_idle) || WE == 2) {
+    const bool block_idle = order && a.env_steps && (a.env_steps[e0] <= 0 || a.n_steps <= 0);
+    if (MODE >= 1 && !block_idle) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
         // the 4 waves for all n_steps steps
-        char* img = simg;
-        auto copy = [&](uint32_t src, uint32_t dst, uint32_t bytes) {
+        char* img = simg0;
+        auto copy_from = [&](const rsrc_t& rsrc, uint32_t src, uint32_t dst, uint32_t bytes) {
             if (MODE == 0 || block_idle) return;
             for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 64u * W * 16u) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, (int)src, 0);
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)o, (int)src, 0);
                 *(uint4*)(img + dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
             }
         };
-        copy(0, 0, SL.tf);
+        auto copy = [&](uint32_t src, uint32_t dst, uint32_t bytes) { copy_from(rs, src, dst, bytes); };
+        if constexpr (MODE == 3) {
+            copy_from(make_rsrc((const char*)a.tab + (size_t)slotA * a.slot_bytes, SL.bytes), 0, 0, SL.tf);
+            copy_from(make_rsrc((const char*)a.tab + (size_t)slotB * a.slot_bytes, SL.bytes), 0, a.lds_img, SL.tf);
+        } else {
+            copy(0, 0, SL.tf);
+        }
         if constexpr (MODE == 2) {   // the kept composite levels at their fixed places (band_solve)
             constexpr uint32_t CB = KL * KL * CE, NL = (uint32_t)mode2_levels(KL);
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
@@ -1236,6 +1094,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
             copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
             copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
         }
+        static_assert(!(FAM == 2 && MODE == 3 && grid_rows_in_lds(R)), "two-slot blocks carry no row constants");
         if constexpr (FAM == 2 && MODE >= 1 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x
             for (int i = threadIdx.x; i < R * 64; i += 64 * W) {
                 const int j = i >> 6, r = (i & 63) * R + j;
@@ -1245,12 +1104,16 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
             }
         }
         if constexpr (FXL) {
-            if (threadIdx.x < 64) {
+            // the H_F force coefficients -cF X of the block's slot (MODE 3: threads 64-127 write slot B's)
+            const bool second = MODE == 3 && threadIdx.x >= 64 && threadIdx.x < 128;
+            if (threadIdx.x < 64 || second) {
+                const double cFs = a.c * a.force[second ? slotB : (MODE == 3 ? slotA : slot)];
+                char* fimg = img + (second ? a.lds_img : 0u) + lds_fx;
 #pragma unroll
                 for (int t = 0; t <= R; ++t) {
                     const int r = lane * R - 1 + t;
                     const double x = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
-                    *(double*)(img + a.lds_fx + t * 512 + lane * 8) = -cFd * x;
+                    *(double*)(fimg + t * 512 + lane * 8) = -cFs * x;
                 }
             }
         }
@@ -1258,15 +1121,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
     }
     if (!active) return;
     const int base = gl * R;
-    // the lane argument of the stencil / reduction / solve helpers: the lane, or the pair context
-    const auto lnv = [&]() {
-        if constexpr (WE == 2) {
-            char* mb = (char*)smem_dyn + (threadIdx.x >> 6) * kPairBytes;
-            return PLane{lane, half, mb, half ? mb - kPairBytes : mb + kPairBytes, 0u};
-        } else {
-            return lane;
-        }
-    }();
+    const int lnv = lane;   // the lane argument of the stencil / reduction / solve helpers
     const int N = a.N;
     Coef<FAM, R, RT> cf;
     load_coef<FAM, R>(cf, a, base);
@@ -1353,7 +1208,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
         const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = (HC ? a.k_dz : sdt * dt * 0.5) * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
-        if (lane == 0 && half == 0) {
+        if (lane == 0) {
             if (a.q_out) a.q_out[(size_t)k * a.B + env] = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = (double)xbar;
         }
@@ -1544,7 +1399,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
             // term7 = A D1, A = H_F^2 (a2 - i a3 H_F - a4 H_F^2 + i a5 H_F^3), Horner in H_F on A/a5
             // (coefficients a_k/a5; a5 applied once in the sum below: no separate i a5 D1 pass)
             auto hf = [&](const cx<RT> (&v)[R], cx<RT> (&u)[R]) {
-                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, a.lds_fx, lnv);
+                if constexpr (FXL) apply_hf_fx<FAM, R>(v, u, cf, tb, lds_fx, lnv);
                 else apply_hf<FAM, R>(v, u, cF, cf, lnv);
             };
             cx<RT> t[R];
@@ -1676,7 +1531,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R, MODE, FAM == 1, WE == 2, LE>(acc, tb, kf, kb, lnv QC_SOLVE_STAMP_PASS);
+        band_solve<KL, R, MODE, FAM == 1, SYMT, LE>(acc, tb, kf, kb, lnv QC_SOLVE_STAMP_PASS);
         QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {
@@ -1699,10 +1554,9 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
                     if (j == jt) suf = s[0];
                 }
                 s[1] = qx.sum();
-                // (lanes of the env: this wave holds env lanes [64 half, 64 half + 63])
-                const int l0 = 64 * half, l1 = (N - 1) / R;
-                if (lt >= l0 && lt < l0 + 64) stop = readlane_d(suf, lt - l0);
-                for (int l = (lt + 1 > l0 ? lt + 1 : l0); l <= l1 && l < l0 + 64; ++l) stop += readlane_d(s[0], l - l0);
+                const int l1 = (N - 1) / R;
+                if (lt < 64) stop = readlane_d(suf, lt);
+                for (int l = lt + 1; l <= l1 && l < 64; ++l) stop += readlane_d(s[0], l);
             } else {
                 double ptop = 0.0, pbot = 0.0;
 #pragma unroll
@@ -1718,14 +1572,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
                 for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
                 for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
             }
-            if constexpr (WE == 2) {   // the pair's norm, next <x> and boundary sum in one exchange
-                wave_sum<2>(s);
-                double u[3] = {s[0], s[1], stop};
-                pl_sum<3>(lnv, u);
-                s[0] = u[0], s[1] = u[1], stop = u[2];
-            } else {
-                step_sum<2>(s);
-            }
+            step_sum<2>(s);
             // 1/sqrt(s0): hardware estimate + two Newton steps (full fp64 precision)
             double scale = __builtin_amdgcn_rsq(s[0]);
             scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
@@ -1766,7 +1613,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
                 gpsi[2 * (wb + j) + 1] = psi[j].im;
             }
     }
-    if (lane == 0 && half == 0) {
+    if (lane == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;
         if (!a.noise) a.ctr[env] = ctr0 + (uint64_t)n_my;   // only the in-kernel Philox stream advances
@@ -1775,7 +1622,7 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
         if constexpr (FAM <= 1) {
             double o[5];
             fock_obs<FAM, R>(psi, cf, lnv, o);
-            if (lane < 5 && half == 0) {
+            if (lane < 5) {
                 double v = o[0];
 #pragma unroll
                 for (int i = 1; i < 5; ++i) v = (lane == i) ? o[i] : v;
@@ -1791,6 +1638,24 @@ __attribute__((amdgpu_waves_per_eu((kBlockWaves<FAM, R, RT, WE> / 4), (kBlockWav
                 a.obs_out[(size_t)env * a.n_obs + lane] = v;
             }
         }
+    }
+}
+
+// The step kernel. DUAL: blocks [0, a.n_mixed) are k_group's two-slot remainder workgroups
+// (a.order_mixed, MODE 3 body), the rest the single-slot workgroups of a.order (MODE body) — one launch,
+// the remainder blocks dispatched first, so the batch fills exactly ceil(B / EPB) workgroups.
+template <int FAM, int R, int MODE, typename RT = double, bool DUAL = false>
+__global__ __launch_bounds__((64 * kStepWaves<FAM, R, RT>))
+__attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM, R, RT> / 4)))) void k_step(
+    const KArgs a) {
+    if constexpr (DUAL) {
+        if (blockIdx.x < a.n_mixed) {
+            step_body<FAM, R, 3, RT>(a, a.order_mixed, blockIdx.x);
+            return;
+        }
+        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x - a.n_mixed);
+    } else {
+        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x);
     }
 }
 
@@ -2056,27 +1921,32 @@ namespace qcart {
 
 static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 
-template <int FAM, int R, int MODE, typename RT, int WE = 1>
+// two-slot remainder workgroups (k_step DUAL): fp64, one wave per env, and two MODE 3 slot images (the
+// tables and the fp64 Fock H_F force coefficients) within the 160 KiB of LDS; the grid kernel whose row
+// constants live in LDS (R >= 17) has no room for a second slot
+template <int FAM, int R, typename RT>
+constexpr uint32_t kDualImg =
+    slot_layout(Fam<FAM>::KL, R, FAM == 1, (uint32_t)sizeof(cx<RT>), slot_sym(FAM != 2, (uint32_t)sizeof(cx<RT>), 64), 64).tf +
+    (FAM <= 1 ? (uint32_t)(R + 1) * 64u * 8u : 0u);
+template <int FAM, int R, typename RT>
+constexpr bool kDual = sizeof(RT) == 8 && !(FAM == 2 && grid_rows_in_lds(R)) && 2u * ((kDualImg<FAM, R, RT> + 15u) & ~15u) <= 160u * 1024u;
+
+template <int FAM, int R, int MODE, typename RT, bool DUAL = false>
 int launch_step_mode(const KArgs& a, hipStream_t st) {
-    const dim3 grid(a.n_blocks), block(64 * kBlockWaves<FAM, R, RT, WE>);
-    constexpr bool lds = MODE >= 1 || WE == 2;
+    const dim3 grid(a.n_blocks + (DUAL ? a.n_mixed : 0u)), block(64 * kStepWaves<FAM, R, RT>);
+    constexpr bool lds = MODE >= 1;
     if (lds) {
         static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
         if (!attr_set) {
-            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE, RT, WE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024) != hipSuccess)
+            if (hipFuncSetAttribute((const void*)k_step<FAM, R, MODE, RT, DUAL>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
                 return -3;
             attr_set = true;
         }
     }
-    hipLaunchKernelGGL((k_step<FAM, R, MODE, RT, WE>), grid, block, lds ? a.lds_bytes : 0, st, a);
+    hipLaunchKernelGGL((k_step<FAM, R, MODE, RT, DUAL>), grid, block, lds ? a.lds_bytes : 0, st, a);
     return 0;
 }
-// (FAM, R, RT) with a two-waves-per-env step kernel: IHO at 2 x 64 lanes x R rows, R = 8 fp64 (N <= 1024)
-// and R = 16 fp32 (N <= 2048, config C5) — each the largest R that runs two waves per SIMD
-template <int FAM, int R, typename RT>
-constexpr bool kHasPair = FAM == 1 && ((R == 8 && sizeof(RT) == 8) || (R == 16 && sizeof(RT) == 4));
-
 // per-family launch entry points, instantiated in qcart_k_{ho,iho,grid,f32}.hip
 template <int FAM, int R, typename RT = double>
 int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rkind, const uint8_t* mask,
@@ -2084,25 +1954,21 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
                void* stream) {
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 4) {   // query: envs per step workgroup
-        if constexpr (kHasPair<FAM, R, RT>)
-            if (a.we == 2) return kBlockWaves<FAM, R, RT, 2> / 2;
-        return a.we == 2 ? -6 : kStepWaves<FAM, R, RT>;
-    }
-    if (kind == 0 && a.we == 2) {
-        if constexpr (kHasPair<FAM, R, RT>) {
-            const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, 2>(a, st)
-                         : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT, 2>(a, st)
-                                           : launch_step_mode<FAM, R, 0, RT, 2>(a, st);
-            if (rc) return rc;
-            return hipGetLastError() == hipSuccess ? 0 : -3;
-        }
-        return -6;
-    }
+    if (kind == 4) return kStepWaves<FAM, R, RT>;   // query: envs per step workgroup
+    if (kind == 6) return kDual<FAM, R, RT> ? (int)((kDualImg<FAM, R, RT> + 15u) & ~15u) : 0;   // query: MODE 3 image
     if (kind == 0) {
-        const int rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT>(a, st)
-                     : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT>(a, st)
-                                       : launch_step_mode<FAM, R, 0, RT>(a, st);
+        int rc;
+        if constexpr (kDual<FAM, R, RT>) {
+            if (a.n_mixed > 0 && a.tab_mode >= 1) {
+                rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, true>(a, st)
+                                     : launch_step_mode<FAM, R, 1, RT, true>(a, st);
+                if (rc) return rc;
+                return hipGetLastError() == hipSuccess ? 0 : -3;
+            }
+        }
+        rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT>(a, st)
+           : a.tab_mode == 1 ? launch_step_mode<FAM, R, 1, RT>(a, st)
+                             : launch_step_mode<FAM, R, 0, RT>(a, st);
         if (rc) return rc;
     }
     else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);

@@ -210,11 +210,10 @@ int build_action(const OpHost& op, double dt, double force, bool mirror, ActHost
             if (r + k < N) act.uc[(size_t)(k - 1) * Np + r] = cm(Wat(r, k), di);
         }
     }
-    // grid (and the two-waves-per-env Fock tables): ab is complex symmetric (H_F real symmetric), so
-    // U[r][r+k] / U[r][r] = L[r+k][r] up to rounding;
-    // the step kernel reads the backward factors from the lc band (SlotLayout sym), so the backward
-    // composites are built from exactly those values
-    if (!op.fock || op.lanes > kWave)
+    // ab is complex symmetric (H_F real symmetric), so U[r][r+k] / U[r][r] = L[r+k][r] up to rounding;
+    // with L D L^T tables (op.sym) the step kernel reads the backward factors from the lc band, so the
+    // backward composites are built from exactly those values
+    if (op.sym)
         for (int k = 1; k <= kl; k++)
             for (int r = 0; r < Np; r++)
                 act.uc[(size_t)(k - 1) * Np + r] = (r + k < Np) ? act.lc[(size_t)(k - 1) * Np + r + k] : cplx(0, 0);

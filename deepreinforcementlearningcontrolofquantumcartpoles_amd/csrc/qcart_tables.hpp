@@ -36,6 +36,7 @@ struct OpHost {
     // step-kernel factor tables: lanes per env and rows per lane (64 x R; 128 x R/2 for the two-waves-
     // per-env step kernel, the same Npad)
     int lanes = 64, Rs = 0;
+    bool sym = false;    // L D L^T tables (slot_sym): the backward factors are read from the lc band
     double w = 1.0;      // dot weight (1 or h)
     double c = 0.0;      // force coupling (omega or pi)
     double h = 0.0;

@@ -255,12 +255,6 @@ int qc_record(qc_handle* h, int32_t read_length, int32_t coarse_grain, double in
  * action a (forward, backward), and the truncation bound used. */
 int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bwd);
 
-/* Waves per env of the handle's step kernel: 1, or 2 when the handle was created with QCART_WE=2 in the
- * environment for an IHO size whose one-wave kernel runs one wave per SIMD (N > 512 fp64, N > 1024 fp32):
- * each env's rows are then split over a wave pair that exchanges halos, sums and scan carries through LDS
- * (opt-in: measured slower). */
-int qc_step_waves_per_env(const qc_handle* h);
-
 /* Deferred input errors: qc_step does not synchronise to validate its actions; an action outside
  * [0, n_slots) of an env with a step budget raises a device error word (the kernels clamp it). This call
  * synchronises the handle's stream, returns QC_EINVAL (message via qc_last_error) if any qc_step since the

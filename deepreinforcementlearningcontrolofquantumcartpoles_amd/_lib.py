@@ -31,7 +31,7 @@ EXPORTS = (
     "qc_env_counters", "qc_set_seed_mt19937", "qc_noise_mode", "qc_mt19937_state", "qc_mt19937_words",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
     "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_record_row_len", "qc_record",
-    "qc_scan_levels", "qc_take_errors", "qc_wavefunction_len", "qc_wavefunction_obs", "qc_set_timing", "qc_step_kernel_time",
+    "qc_scan_levels", "qc_take_errors", "qc_step_group_size", "qc_group_layout", "qc_wavefunction_len", "qc_wavefunction_obs", "qc_set_timing", "qc_step_kernel_time",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
     "qc_mactor_create", "qc_mactor_destroy", "qc_mactor_last_error", "qc_mactor_set_stream", "qc_mactor_noise_len",
@@ -189,6 +189,8 @@ def lib() -> ctypes.CDLL:
     L.qc_wavefunction_len.argtypes = [vp]
     L.qc_wavefunction_obs.argtypes = [vp, vp, d, vp]
     L.qc_scan_levels.argtypes = [vp, i32, P(i32), P(i32)]
+    L.qc_step_group_size.argtypes = [vp]
+    L.qc_group_layout.argtypes = [vp, vp, i64, vp, i64]
     for name in ("qc_take_errors",):   # (older in-tree builds in A/B runs lack them)
         if hasattr(L, name):
             getattr(L, name).argtypes = [vp]

@@ -159,6 +159,17 @@ class Stepper:
         self.n_slots = max(self.n_slots, slot + 1)
         return slot
 
+    def group_layout(self):
+        """(single-slot workgroups, two-slot workgroups) of the last grouped step() call: int32 numpy arrays
+        [n][envs per workgroup] of env ids, -1 = idle wave (qc_group_layout; synchronises)."""
+        import numpy as np
+        g = int(L.lib().qc_step_group_size(self._h))
+        order = np.full(((self.batch + g - 1) // g + 65) * g, -1, np.int32)
+        mixed = np.full(64 * g, -1, np.int32)
+        n_mixed = L.check(L.lib().qc_group_layout(self._h, order.ctypes.data, order.size, mixed.ctypes.data,
+                                                  mixed.size), self._h)
+        return order.reshape(-1, g), mixed[:n_mixed * g].reshape(-1, g)
+
     def scan_levels(self, action: int):
         f, b = ctypes.c_int32(), ctypes.c_int32()
         L.check(L.lib().qc_scan_levels(self._h, action, ctypes.byref(f), ctypes.byref(b)), self._h)

@@ -249,6 +249,8 @@ KArgs base_args(const qc_handle* h) {
             a.lds_img = h->dual_img;
             a.lds_bytes = std::max(a.lds_bytes, 2u * h->dual_img);
         }
+        if (const char* e = std::getenv("QCART_LDS_MIN"))   // diagnostic: pad the dynamic LDS
+            if (mode >= 1) a.lds_bytes = std::max(a.lds_bytes, (uint32_t)std::atoi(e));
     }
     a.precision = p.precision;
     a.order = nullptr;
@@ -585,7 +587,7 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         // two-slot remainder workgroups when the step kernel has them (tables in LDS, fp64, one wave per env)
         const bool dual = a.lds_img > 0;
         if (dual && !h->d_order_mixed) {
-            hipError_t e = hipMalloc((void**)&h->d_order_mixed, (size_t)kMaxSlots * W * sizeof(int32_t));
+            hipError_t e = hipMalloc((void**)&h->d_order_mixed, ((size_t)kMaxSlots * W + 1) * sizeof(int32_t));
             if (e != hipSuccess) return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
         }
         if (launch_group(actions, default_action, env_steps, n_steps, h->p.batch, (int)h->acts.size(), (int)W,
@@ -595,6 +597,8 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         a.n_blocks = (uint32_t)(cap / W);
         a.order_mixed = dual ? h->d_order_mixed : nullptr;
         a.n_mixed = dual ? (uint32_t)h->acts.size() : 0u;
+        a.n_mixed_used = dual ? h->d_order_mixed + h->acts.size() * W : nullptr;
+        if (const char* e = std::getenv("QCART_DUAL_PLAIN")) a.dbg_plain = std::atoi(e);
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (h->timing) {
@@ -806,6 +810,26 @@ int qc_wavefunction_obs(qc_handle* h, const void* psi, double input_scaling, flo
     int rc = launch_wavefunction(psi, h->p.precision, h->p.batch, h->op.N, lo, rows, input_scaling, out,
                                  h->stream);
     return rc ? fail(h, QC_EHIP, "wavefunction kernel launch failed") : QC_OK;
+}
+
+int qc_step_group_size(const qc_handle* h) { return h ? h->wpb : QC_EINVAL; }
+
+int qc_group_layout(qc_handle* h, int32_t* order, int64_t order_len, int32_t* mixed, int64_t mixed_len) {
+    if (!h) return QC_EINVAL;
+    DeviceGuard g(h->device);
+    if (hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize")) return QC_EHIP;
+    if (order && order_len > 0 && h->d_order) {
+        const size_t n = std::min((size_t)order_len, h->order_cap);
+        if (hip_check(h, hipMemcpy(order, h->d_order, n * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
+            return QC_EHIP;
+    }
+    const int64_t mcap = h->d_order_mixed ? (int64_t)kMaxSlots * h->wpb : 0;
+    if (mixed && mixed_len > 0 && mcap > 0) {
+        const size_t n = (size_t)std::min(mixed_len, mcap);
+        if (hip_check(h, hipMemcpy(mixed, h->d_order_mixed, n * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
+            return QC_EHIP;
+    }
+    return h->d_order_mixed ? (int)h->acts.size() : 0;
 }
 
 int qc_take_errors(qc_handle* h) {

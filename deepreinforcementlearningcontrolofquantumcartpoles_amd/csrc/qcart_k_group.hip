@@ -100,8 +100,10 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
     if (last_big >= 0)   // the packed region's last, partial workgroup
         for (int p = packed_end + t; p < (packed_end + g - 1) / g * g; p += blockDim.x) *packed_dst(last_big, p) = -1;
     for (int i = total + t; i < cap; i += blockDim.x) order[i] = -1;
-    if (order_mixed)
+    if (order_mixed) {
         for (int i = n_mix * g + t; i < n_slots * g; i += blockDim.x) order_mixed[i] = -1;
+        if (t == 0) order_mixed[n_slots * g] = n_mix;   // k_step DUAL: the two-slot blocks come first
+    }
 }
 
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,

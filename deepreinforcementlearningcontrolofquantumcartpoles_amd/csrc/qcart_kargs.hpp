@@ -80,7 +80,9 @@ struct KArgs {
     const int32_t* order;      // [n_blocks*W] envs grouped by force slot (-1 idle) or null (identity)
     uint32_t n_blocks;         // step kernel grid (single-slot workgroups)
     const int32_t* order_mixed;   // [n_mixed*W] k_group's two-slot remainder workgroups (-1 idle)
-    uint32_t n_mixed;          // two-slot blocks ahead of the n_blocks (0: none; launch_step DUAL)
+    uint32_t n_mixed;          // capacity of two-slot blocks (0: none; launch_step DUAL); grid n_mixed + n_blocks
+    const int32_t* n_mixed_used;   // device: k_group's two-slot workgroup count (blocks [0, it) run them)
+    int32_t dbg_plain;         // diagnostic (QCART_DUAL_PLAIN=1): the plain kernel on the packed layout
     uint32_t lds_img;          // bytes of one slot's MODE 3 image (tables + H_F force coefficients)
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
@@ -153,8 +155,9 @@ bool have_kernel(int family, int R, int precision = 0);
 int step_waves(int family, int R, int precision = 0);   // envs per step-kernel workgroup (<0: none)
 int step_dual_img(int family, int R, int precision = 0);   // MODE 3 slot-image bytes (0: no two-slot blocks)
 // envs grouped by force slot into order[cap] (gran-aligned groups, -1 padding); qcart_k_group.hip
-// order_mixed (optional, [n_slots * gran]): slots with >= gran envs are laid out back to back and cut into
-// gran-env workgroups; the ones that straddle two slots go to order_mixed (k_step DUAL), the rest to order
+// order_mixed (optional, [n_slots * gran] + 1 count word): slots with >= gran envs are laid out back to back
+// and cut into gran-env workgroups; the ones that straddle two slots go to order_mixed (k_step DUAL), the rest
+// to order, and their number to order_mixed[n_slots * gran]
 int launch_group(const int32_t* actions, int32_t default_action, const int32_t* env_steps, int32_t n_steps, int64_t B,
                  int n_slots, int gran, int32_t* order, int32_t cap, int32_t* bad, int32_t* order_mixed, void* stream);
 

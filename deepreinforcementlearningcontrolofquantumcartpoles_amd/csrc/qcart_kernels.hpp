@@ -1129,7 +1129,12 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     RT* gpsi = (RT*)a.psi + (size_t)env * N * 2;
     cx<RT> psi[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld(gpsi, base + j) : C(RT(0), RT(0));
+    // psi streams through once per launch: non-temporal loads and stores, so it does not evict what the L2
+    // should keep (the slot tables, and the scratch lines of the kernels that spill)
+    for (int j = 0; j < R; ++j)
+        psi[j] = (base + j < N) ? C(__builtin_nontemporal_load(gpsi + 2 * (base + j)),
+                                    __builtin_nontemporal_load(gpsi + 2 * (base + j) + 1))
+                                : C(RT(0), RT(0));
 
     const bool win_on = a.win_hi > a.win_lo;
     // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)
@@ -1169,16 +1174,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         xbar = (RT)(a.w * s[0]);                                  // x_expct (IHO:197-203, QO:230-236)
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
-    const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
-    // uniform step constants: host-folded kernel arguments (SGPRs) for the Fock kernels, where device-side
-    // they were VGPR values the register allocator spilled (metric: 35 spilled registers -> 0, -1.7 %); the
-    // grid kernels keep the device-side forms (their schedule measured 2-3 % faster that way). Same values.
+    // uniform step constants: host-folded kernel arguments for the Fock kernels, where device-side they were
+    // VGPR values the register allocator spilled (metric: 35 spilled registers -> 0, -1.7 %); the grid kernels
+    // keep the device-side forms (their schedule measured 2-3 % faster that way). Same values. (Read in the
+    // step loop, below.)
     constexpr bool HC = FAM != 2;
-    const double inv_sdt = HC ? a.inv_sdt : 1.0 / sdt, inv_dt = HC ? a.inv_dt : 1.0 / dt;
-    // vector-facing constants at the working precision
-    const RT g4r = (RT)g4, dtr = (RT)dt, a5r = (RT)a.a5;
-    const RT b2r = (RT)(HC ? a.b2 : a.a2 / a.a5), b3r = (RT)(HC ? a.b3 : a.a3 / a.a5),
-             b4r = (RT)(HC ? a.b4 : a.a4 / a.a5);   // term7 Horner coefficients / a5
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     double nz0 = 0.0, nz1 = 0.0;
 
@@ -1193,6 +1193,20 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     const uint64_t ctr0 = a.ctr[env];
     QC_STAMP_BEGIN();
     for (int k = 0; k < n_my; ++k) {
+        // the loop's uniform constants are re-read from the kernarg segment every step (s_load through the
+        // scalar cache; the opaque pointer keeps the compiler from hoisting them) instead of held in SGPRs
+        // across the loop: at 106 SGPRs the metric kernel spilled ~90 of them into VGPR lanes (v_writelane /
+        // v_readlane on the VALU every step) and 3 VGPRs to scratch; now 92 SGPRs, no spill (loop 2 880 ->
+        // 2 774 instructions)
+        using CK = const __attribute__((address_space(4))) KArgs;
+        CK* kap = (CK*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kap));
+        CK& a = *kap;   // (shadows the parameter inside the step)
+        const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
+        const double inv_sdt = HC ? a.inv_sdt : 1.0 / sdt, inv_dt = HC ? a.inv_dt : 1.0 / dt;
+        const RT g4r = (RT)g4, dtr = (RT)dt, a5r = (RT)a.a5;
+        const RT b2r = (RT)(HC ? a.b2 : a.a2 / a.a5), b3r = (RT)(HC ? a.b3 : a.a3 / a.a5),
+                 b4r = (RT)(HC ? a.b4 : a.a4 / a.a5);
         QC_STAMP(0);
         if ((k & 63) == 0) {   // lane j: normals of step k + j
             if (a.noise) {
@@ -1609,8 +1623,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
 #pragma unroll
         for (int j = 0; j < R; ++j)
             if (wb + j < N) {
-                gpsi[2 * (wb + j)] = psi[j].re;
-                gpsi[2 * (wb + j) + 1] = psi[j].im;
+                __builtin_nontemporal_store(psi[j].re, gpsi + 2 * (wb + j));
+                __builtin_nontemporal_store(psi[j].im, gpsi + 2 * (wb + j) + 1);
             }
     }
     if (lane == 0) {
@@ -1641,19 +1655,23 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     }
 }
 
-// The step kernel. DUAL: blocks [0, a.n_mixed) are k_group's two-slot remainder workgroups
-// (a.order_mixed, MODE 3 body), the rest the single-slot workgroups of a.order (MODE body) — one launch,
-// the remainder blocks dispatched first, so the batch fills exactly ceil(B / EPB) workgroups.
+// The step kernel. DUAL: blocks [0, m) are k_group's m two-slot remainder workgroups (a.order_mixed, MODE 3
+// body), the next ones the single-slot workgroups of a.order (MODE body) — one launch whose busy blocks are
+// contiguous from 0 (blocks are dealt round-robin to the 8 XCDs: an idle block in the middle would shift a
+// workgroup onto another XCD and cost that XCD an extra round), so the batch fills ceil(B / EPB) workgroups.
 template <int FAM, int R, int MODE, typename RT = double, bool DUAL = false>
 __global__ __launch_bounds__((64 * kStepWaves<FAM, R, RT>))
 __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM, R, RT> / 4)))) void k_step(
     const KArgs a) {
     if constexpr (DUAL) {
-        if (blockIdx.x < a.n_mixed) {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(*a.n_mixed_used);
+        if (blockIdx.x < m) {
+#ifndef QCART_TMP_NOBODY
             step_body<FAM, R, 3, RT>(a, a.order_mixed, blockIdx.x);
+#endif
             return;
         }
-        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x - a.n_mixed);
+        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x - m);
     } else {
         step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x);
     }
@@ -1959,7 +1977,7 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     if (kind == 0) {
         int rc;
         if constexpr (kDual<FAM, R, RT>) {
-            if (a.n_mixed > 0 && a.tab_mode >= 1) {
+            if (a.n_mixed > 0 && a.tab_mode >= 1 && !a.dbg_plain) {
                 rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, true>(a, st)
                                      : launch_step_mode<FAM, R, 1, RT, true>(a, st);
                 if (rc) return rc;

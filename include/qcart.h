@@ -261,6 +261,13 @@ int qc_scan_levels(const qc_handle* h, int32_t action, int32_t* fwd, int32_t* bw
  * last call saw such an action, and clears the word; QC_OK otherwise. */
 int qc_take_errors(qc_handle* h);
 
+/* Introspection (tests, diagnostics): the workgroup layout of the last grouped qc_step call (k_group).
+ * Copies up to order_len entries of the single-slot workgroup list and up to mixed_len of the two-slot list
+ * (workgroups of qc_step_group_size() envs each, -1 = idle wave) into host buffers (either may be NULL) and
+ * returns the number of two-slot workgroup slots (0 when the handle does not use them). Synchronises. */
+int qc_step_group_size(const qc_handle* h);
+int qc_group_layout(qc_handle* h, int32_t* order, int64_t order_len, int32_t* mixed, int64_t mixed_len);
+
 /* ---------------------------------------------------------------------------------------------
  * Batched DQN actor: the reference's direct_DQN action selection
  * (inverted harmonic oscillator/RL.py:80-111 + layers.py FactorizedNoisy / Linear_weight_normalize),

@@ -462,6 +462,49 @@ def test_two_slot_workgroups_bitwise_equal(monkeypatch, case, mode):
     assert torch.equal(outs[0][3][ran], outs[1][3][ran])
 
 
+@pytest.mark.parametrize("B", [4096, 203])
+def test_group_layout_packs_slots(B):
+    """k_group's layout (qc_group_layout): every env with a step budget in exactly one workgroup; each
+    single-slot workgroup holds one slot; each two-slot workgroup exactly two; slots of >= 8 envs fill
+    ceil(their total / 8) workgroups; smaller slots and the no-budget envs are padded on their own."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)
+    rng = np.random.default_rng(B)
+    acts = rng.integers(0, 21, B).astype(np.int32)
+    if B < 1000:   # one slot of exactly 9 envs, one of 2
+        acts[acts == 3] = 4
+        acts[:9] = 3
+        acts[acts == 6] = 5
+        acts[9:11] = 6
+    budget = np.full(B, 80, np.int32)
+    budget[rng.choice(B, B // 20, replace=False)] = 0
+    st = Stepper(ph, B, 0, seed=1)
+    psi = st.new_state()
+    st.reset(psi, 1, arg0=4)
+    st.step(psi, torch.from_numpy(acts).cuda(), 2, env_steps=torch.from_numpy(budget).cuda())
+    order, mixed = st.group_layout()
+    g = order.shape[1]
+    mixed = np.array([wg for wg in mixed if (wg >= 0).any()]).reshape(-1, g)
+    assert len(mixed) > 0
+    seen = np.concatenate([order.ravel(), mixed.ravel()])
+    seen = seen[seen >= 0]
+    assert sorted(seen.tolist()) == list(range(B))
+    ran = budget > 0
+    slot = np.where(ran, acts, 99)
+    for wg in order:
+        e = wg[wg >= 0]
+        assert len(set(slot[e].tolist())) <= 1
+    for wg in mixed:
+        e = wg[wg >= 0]
+        assert len(set(slot[e].tolist())) == 2 and ran[e].all()
+    cnt = np.bincount(acts[ran], minlength=21)
+    big, small = cnt[cnt >= g].sum(), cnt[(cnt > 0) & (cnt < g)]
+    busy = [wg for wg in order if (wg >= 0).any()]
+    n_nobudget = (B - ran.sum() + g - 1) // g
+    assert len(busy) + len(mixed) == (big + g - 1) // g + len(small) + n_nobudget
+    print(f"B={B}: {len(busy)} single-slot + {len(mixed)} two-slot workgroups "
+          f"(padded per slot: {int(sum((c + g - 1) // g for c in cnt if c)) + n_nobudget})")
+
+
 @pytest.mark.parametrize("config", ["C2", "C3", "C4", "metric"])
 def test_config_size_batch_properties(oracle_mod, config):
     """At a BASELINE config's full per-GPU batch (C2: IHO N=512 B=4096; C3: QO x_n=1025, B=16384; C4: IQO

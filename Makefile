@@ -16,8 +16,10 @@ all: $(LIB) oracle
 # kernel TUs: MachineLICM off — it hoists loop-invariant FP64 constants of the step loop's rare
 # noise refill into registers that then spill (same speed, ~0.9 GB less scratch traffic per launch)
 KFLAGS ?= -mllvm -disable-machine-licm
-# (the grid TU keeps LICM: its 9-band loop-invariant addressing is worth hoisting, measured +12 %)
-$(CSRC)/build/qcart_k_grid.o: KFLAGS :=
+# (the grid TU keeps LICM: its 9-band loop-invariant addressing is worth hoisting, measured +12 %; and
+# contracts across statements: C3 -3 % against -ffp-contract=on, its table placements and two-slot
+# workgroups still bit-identical — tests/test_gpu_parity.py checks both)
+$(CSRC)/build/qcart_k_grid.o: KFLAGS := -ffp-contract=fast
 # fp32 TU: complex values as packed 2-lane vectors (QCART_F32_PACKED, explicit v_pk_* arithmetic; MS property
 # accessors keep .re/.im) and no SLP packing of the remaining scalar code (it would reshuffle the pairs)
 $(CSRC)/build/qcart_k_f32.o: KFLAGS += -fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED

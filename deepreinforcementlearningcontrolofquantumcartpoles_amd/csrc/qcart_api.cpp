@@ -249,8 +249,6 @@ KArgs base_args(const qc_handle* h) {
             a.lds_img = h->dual_img;
             a.lds_bytes = std::max(a.lds_bytes, 2u * h->dual_img);
         }
-        if (const char* e = std::getenv("QCART_LDS_MIN"))   // diagnostic: pad the dynamic LDS
-            if (mode >= 1) a.lds_bytes = std::max(a.lds_bytes, (uint32_t)std::atoi(e));
     }
     a.precision = p.precision;
     a.order = nullptr;
@@ -598,7 +596,6 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         a.order_mixed = dual ? h->d_order_mixed : nullptr;
         a.n_mixed = dual ? (uint32_t)h->acts.size() : 0u;
         a.n_mixed_used = dual ? h->d_order_mixed + h->acts.size() * W : nullptr;
-        if (const char* e = std::getenv("QCART_DUAL_PLAIN")) a.dbg_plain = std::atoi(e);
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (h->timing) {

@@ -82,7 +82,6 @@ struct KArgs {
     const int32_t* order_mixed;   // [n_mixed*W] k_group's two-slot remainder workgroups (-1 idle)
     uint32_t n_mixed;          // capacity of two-slot blocks (0: none; launch_step DUAL); grid n_mixed + n_blocks
     const int32_t* n_mixed_used;   // device: k_group's two-slot workgroup count (blocks [0, it) run them)
-    int32_t dbg_plain;         // diagnostic (QCART_DUAL_PLAIN=1): the plain kernel on the packed layout
     uint32_t lds_img;          // bytes of one slot's MODE 3 image (tables + H_F force coefficients)
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;

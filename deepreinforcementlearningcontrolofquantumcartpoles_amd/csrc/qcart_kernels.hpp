@@ -1013,6 +1013,20 @@ constexpr int kStepWaves =
     ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= QCART_W8_MAX_RG)) ? 8 : 4;
 
 
+// The step loop's view of the kernel arguments (KAR: the kernarg segment through a pointer made opaque
+// every step, so its loads are not hoisted out of the loop; otherwise the by-value parameter itself)
+template <bool KAR>
+__device__ __forceinline__ decltype(auto) step_kargs(const KArgs& a) {
+    if constexpr (KAR) {
+        using CK = const __attribute__((address_space(4))) KArgs;
+        CK* kap = (CK*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kap));
+        return (*kap);
+    } else {
+        return (a);
+    }
+}
+
 // MODE 3: a two-slot block (k_group's remainder workgroups, KArgs::order_mixed): MODE 1 reads (tables in
 // LDS, scan composites from the slot's global block) with both slots' images in LDS, a.lds_img bytes apart;
 // every wave uses its own env's slot and image
@@ -1191,17 +1205,17 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
+    constexpr bool KAR = !(FAM == 2 && R >= 17) && !(sizeof(RT) == 4 && R >= 32);
+    const KArgs& a_in = a;
     QC_STAMP_BEGIN();
     for (int k = 0; k < n_my; ++k) {
-        // the loop's uniform constants are re-read from the kernarg segment every step (s_load through the
-        // scalar cache; the opaque pointer keeps the compiler from hoisting them) instead of held in SGPRs
+        // KAR: the loop's uniform constants are re-read from the kernarg segment every step (s_load through
+        // the scalar cache; the opaque pointer keeps the compiler from hoisting them) instead of held in SGPRs
         // across the loop: at 106 SGPRs the metric kernel spilled ~90 of them into VGPR lanes (v_writelane /
         // v_readlane on the VALU every step) and 3 VGPRs to scratch; now 92 SGPRs, no spill (loop 2 880 ->
-        // 2 774 instructions)
-        using CK = const __attribute__((address_space(4))) KArgs;
-        CK* kap = (CK*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(kap));
-        CK& a = *kap;   // (shadows the parameter inside the step)
+        // 2 774 instructions). Not for the kernels that spill VGPRs to scratch anyway (grid R = 17, fp32
+        // R = 32), where the per-step loads cost more than they save (C3 198 -> 218 ms per episode)
+        const auto& a = step_kargs<KAR>(a_in);   // (shadows the parameter inside the step)
         const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
         const double inv_sdt = HC ? a.inv_sdt : 1.0 / sdt, inv_dt = HC ? a.inv_dt : 1.0 / dt;
         const RT g4r = (RT)g4, dtr = (RT)dt, a5r = (RT)a.a5;
@@ -1666,11 +1680,11 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     if constexpr (DUAL) {
         const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(*a.n_mixed_used);
         if (blockIdx.x < m) {
-#ifndef QCART_TMP_NOBODY
             step_body<FAM, R, 3, RT>(a, a.order_mixed, blockIdx.x);
-#endif
             return;
         }
+        // the grid has n_mixed - m more blocks than a.order holds
+        if (blockIdx.x - m >= a.n_blocks) return;
         step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x - m);
     } else {
         step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x);
@@ -1977,7 +1991,7 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     if (kind == 0) {
         int rc;
         if constexpr (kDual<FAM, R, RT>) {
-            if (a.n_mixed > 0 && a.tab_mode >= 1 && !a.dbg_plain) {
+            if (a.n_mixed > 0 && a.tab_mode >= 1) {
                 rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, true>(a, st)
                                      : launch_step_mode<FAM, R, 1, RT, true>(a, st);
                 if (rc) return rc;

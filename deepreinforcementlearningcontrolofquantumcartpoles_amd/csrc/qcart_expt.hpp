@@ -8,7 +8,7 @@
 
 #ifdef QCART_STAMPS
 namespace qcart {
-__device__ unsigned long long qc_stamps[16];
+__device__ unsigned long long qc_stamps[20];
 }
 #define QC_STAMP(ph)                                                                                 \
     do {                                                                                             \
@@ -24,7 +24,23 @@ __device__ unsigned long long qc_stamps[16];
 #define QC_STAMP_BEGIN()                                                                             \
     unsigned long long st_acc[16] = {0}, st_t = 0;                                                   \
     int st_ph = 9;                                                                                   \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory")
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");                     \
+    const unsigned long long st_loop0 = st_t
+// wave entry (k_step) and exit (after the write-back): slots 16 (entry -> loop), 17 (loop end -> exit),
+// 18 (wave count)
+#define QC_KSTAMP_ENTRY()                                                                            \
+    unsigned long long kst_t0;                                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(kst_t0)::"memory")
+#define QC_KSTAMP_EXIT(lane)                                                                         \
+    do {                                                                                             \
+        unsigned long long t_;                                                                       \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+        if ((lane) == 0) {                                                                           \
+            atomicAdd(&qc_stamps[16], st_loop0 - kst_t0);                                            \
+            atomicAdd(&qc_stamps[17], t_ - st_t);                                                    \
+            atomicAdd(&qc_stamps[18], 1ull);                                                         \
+        }                                                                                            \
+    } while (0)
 #define QC_STAMP_END(lane)                                                                           \
     do {                                                                                             \
         QC_STAMP(9);                                                                                 \
@@ -37,8 +53,8 @@ __device__ unsigned long long qc_stamps[16];
 
 // read and clear the per-phase cycle sums (weak: an experiment build stamps one family TU)
 extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qcart::qc_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    unsigned long long z[16] = {0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qcart::qc_stamps), sizeof(unsigned long long) * 20) != hipSuccess) return -1;
+    unsigned long long z[20] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(qcart::qc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #else
@@ -50,6 +66,12 @@ extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
     } while (0)
 #define QC_STAMP_END(lane) \
     do {                   \
+    } while (0)
+#define QC_KSTAMP_ENTRY() \
+    do {                  \
+    } while (0)
+#define QC_KSTAMP_EXIT(lane) \
+    do {                     \
     } while (0)
 #define QC_SOLVE_STAMP_ARGS
 #define QC_SOLVE_STAMP_PASS

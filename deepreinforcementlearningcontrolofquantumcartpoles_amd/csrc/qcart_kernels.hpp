@@ -1032,6 +1032,7 @@ __device__ __forceinline__ decltype(auto) step_kargs(const KArgs& a) {
 // every wave uses its own env's slot and image
 template <int FAM, int R, int MODE, typename RT>
 __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, const uint32_t blk) {
+    QC_KSTAMP_ENTRY();
     constexpr int KL = Fam<FAM>::KL;
     constexpr int W = kStepWaves<FAM, R, RT>;   // waves per block
     constexpr int EPB = W;                      // envs per block (one wave per env)
@@ -1667,6 +1668,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             }
         }
     }
+    QC_KSTAMP_EXIT(lane);
 }
 
 // The step kernel. DUAL: blocks [0, m) are k_group's m two-slot remainder workgroups (a.order_mixed, MODE 3

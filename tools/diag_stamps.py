@@ -39,17 +39,20 @@ def main():
     L = _lib.lib()
     f = L.qc_debug_stamps
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 20)()
     st.step(psi, acts, 80)
     torch.cuda.synchronize()
     f(buf)
     st.step(psi, acts, 80)
     torch.cuda.synchronize()
     f(buf)
-    tot = sum(buf)
+    tot = sum(buf[:16])
     print(f"family {ph.family} N={ph.dim} a_mode={a_mode} B={B}: total {tot / (B * 80):.0f} cycles per wave-step (stamped build)")
-    for name, v in zip(PHASES, buf):
+    for name, v in zip(PHASES, buf[:16]):
         print(f"  {name:10s} {v / (B * 80):8.0f} cyc  {100 * v / tot:5.1f} %")
+    nw = max(1, buf[18])
+    print(f"  per wave: entry -> loop {buf[16] / nw:.0f} cyc, loop end -> exit {buf[17] / nw:.0f} cyc, "
+          f"loop {tot / nw:.0f} cyc ({nw} waves)")
 
 
 if __name__ == "__main__":

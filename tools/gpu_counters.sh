@@ -1,15 +1,17 @@
 #!/bin/bash
 # SQ issue/stall counters for the step kernel (separate PMC passes; no trace domains combined).
+# usage: tools/gpu_counters.sh TAG [CONFIG]
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-r01}"
+CONFIG="${2:-metric}"   # bench.py --config
 mkdir -p "$ROOT/gpurun_out"
 cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
   timeout -k 10 600 rocprofv3 --pmc "$@" --kernel-include-regex k_step --output-format csv \
      -d "$ROOT/gpurun_out/prof_${name}_$TAG" -o run \
-     -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$ROOT/gpurun_out/prof_${name}_$TAG.log" 2>&1
+     -- python3 "$ROOT/bench.py" --config "$CONFIG" --steps 2 --warmup 1 --no-cpu-baseline > "$ROOT/gpurun_out/prof_${name}_$TAG.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   return $rc

@@ -758,11 +758,41 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
         for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], P[i * KL + k], c[k]);
 }
 
+// One substitution pass over the lane's rows (FWD: 0 -> R-1, else R-1 -> 0): ld(j, q) reads row j's
+// NQ factors into q, body(j, q) consumes them. PD > 0: the reads run PD rows ahead of the row being
+// solved — the pass is a chain of dependent FMAs from row to row, and at one wave per SIMD a factor read
+// issued just before its use stalls the wave for the LDS latency on every row. The sched_barrier keeps
+// the reads where they are issued (VALU / SALU may move across it).
+template <int R, int NQ, int PD, bool FWD, typename RT, typename LD, typename BODY>
+__device__ __forceinline__ void solve_rows(LD&& ld, BODY&& body) {
+    if constexpr (PD == 0) {
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            const int j = FWD ? t : R - 1 - t;
+            cx<RT> q[NQ];
+            ld(j, q);
+            body(j, q);
+        }
+    } else {
+        cx<RT> q[PD + 1][NQ];
+#pragma unroll
+        for (int t = 0; t < PD; ++t)
+            if (t < R) ld(FWD ? t : R - 1 - t, q[t]);
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            if (t + PD < R) ld(FWD ? t + PD : R - 1 - (t + PD), q[(t + PD) % (PD + 1)]);
+            __builtin_amdgcn_sched_barrier(0x0006);
+            body(FWD ? t : R - 1 - t, q[t % (PD + 1)]);
+        }
+    }
+}
+
 // Composite level offsets: forward level l at f0 + l*C, row prefix at fP; backward at b0 + l*C, bP
 // (C = kl*kl*1024 bytes). Global block: f0 = SL.tf, fP = level 6; LDS image: the kept levels packed.
 // SYM (grid): the backward factor U[r][r+1+k] / U[r][r] is read as L[r+1+k][r] from the lc band (row
 // r + 1 + k: the same lane's run, or a following lane's — dl elements further — past the lane's rows).
-template <int KL, int R, int MODE, bool M2, bool SYM, int LE, typename RT, typename LT>
+// PD: solve_rows' read-ahead distance (0 for two waves per SIMD, whose partner wave covers the latency)
+template <int KL, int R, int MODE, bool M2, bool SYM, int LE, int PD, typename RT, typename LT>
 __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& tb, int kf, int kb,
                                            const LT& lane QC_SOLVE_STAMP_ARGS) {
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
@@ -788,16 +818,22 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     cx<RT> s[KL];
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(RT(0), RT(0));
+
+    solve_rows<R, KL, PD, true, RT>(
+        [&](int j, cx<RT> (&q)[KL]) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-        cx<RT> y = b[j];
+            for (int k = 0; k < KL; ++k)
+                if (k < j) q[k] = tb.c(SL.lc + (uint32_t)(k * R + j) * CE);
+        },
+        [&](int j, const cx<RT> (&q)[KL]) {
+            cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k)   // s[k] = y_{j-1-k}: zero for k >= j (no multiplies by 0)
-            if (k < j) y = cmsub(y, tb.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
+            for (int k = KL - 1; k >= 0; --k)   // s[k] = y_{j-1-k}: zero for k >= j (no multiplies by 0)
+                if (k < j) y = cmsub(y, q[k], s[k]);
 #pragma unroll
-        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
-        s[0] = y;
-    }
+            for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+            s[0] = y;
+        });
     QC_STAMP(10);
     if (hf) {
         scan_rows<KL, true, MODE, LE>(s, tb, f0, fP, kf);
@@ -827,31 +863,41 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     // incoming state from lane - 1, pass 2
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shr1(s[k].re), shr1(s[k].im));
+    solve_rows<R, KL, PD, true, RT>(
+        [&](int j, cx<RT> (&q)[KL]) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-        cx<RT> y = b[j];
+            for (int k = 0; k < KL; ++k) q[k] = tb2.c(SL.lc + (uint32_t)(k * R + j) * CE);
+        },
+        [&](int j, const cx<RT> (&q)[KL]) {
+            cx<RT> y = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) y = cmsub(y, tb2.c(SL.lc + (uint32_t)(k * R + j) * CE), s[k]);
+            for (int k = KL - 1; k >= 0; --k) y = cmsub(y, q[k], s[k]);
 #pragma unroll
-        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
-        s[0] = y;
-        b[j] = y;
-    }
+            for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+            s[0] = y;
+            b[j] = y;
+        });
     QC_STAMP(12);
     // backward, pass 1 (rows high -> low): x_r = dinv_r y_r - sum_k uc_k x_{r+k}
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(RT(0), RT(0));
+    solve_rows<R, KL + 1, PD, false, RT>(
+        [&](int j, cx<RT> (&q)[KL + 1]) {
+            q[KL] = tb.c(SL.di + (uint32_t)j * CE);
 #pragma unroll
-    for (int j = R - 1; j >= 0; --j) {
-        b[j] = cmul(tb.c(SL.di + (uint32_t)j * CE), b[j]);   // D^-1 y, reused by pass 2
-        cx<RT> x = b[j];
+            for (int k = 0; k < KL; ++k)
+                if (j + k < R - 1) q[k] = ucf(tb, k, j);
+        },
+        [&](int j, const cx<RT> (&q)[KL + 1]) {
+            b[j] = cmul(q[KL], b[j]);   // D^-1 y, reused by pass 2
+            cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k)   // s[k] = x_{j+1+k}: zero for j + k >= R - 1
-            if (j + k < R - 1) x = cmsub(x, ucf(tb, k, j), s[k]);
+            for (int k = KL - 1; k >= 0; --k)   // s[k] = x_{j+1+k}: zero for j + k >= R - 1
+                if (j + k < R - 1) x = cmsub(x, q[k], s[k]);
 #pragma unroll
-        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
-        s[0] = x;
-    }
+            for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+            s[0] = x;
+        });
     QC_STAMP(13);
     if (hb) {
         scan_rows<KL, false, MODE, LE>(s, tb, b0, bP, kb);
@@ -877,16 +923,20 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     if constexpr (KL == 4) asm volatile("" : "+v"(tb3.vc), "+v"(tb3.hc));
 #pragma unroll
     for (int k = 0; k < KL; ++k) s[k] = C(shl1(s[k].re), shl1(s[k].im));
+    solve_rows<R, KL, PD, false, RT>(
+        [&](int j, cx<RT> (&q)[KL]) {
 #pragma unroll
-    for (int j = R - 1; j >= 0; --j) {
-        cx<RT> x = b[j];
+            for (int k = 0; k < KL; ++k) q[k] = ucf(tb3, k, j);
+        },
+        [&](int j, const cx<RT> (&q)[KL]) {
+            cx<RT> x = b[j];
 #pragma unroll
-        for (int k = KL - 1; k >= 0; --k) x = cmsub(x, ucf(tb3, k, j), s[k]);
+            for (int k = KL - 1; k >= 0; --k) x = cmsub(x, q[k], s[k]);
 #pragma unroll
-        for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
-        s[0] = x;
-        b[j] = x;
-    }
+            for (int k = KL - 1; k > 0; --k) s[k] = s[k - 1];
+            s[0] = x;
+            b[j] = x;
+        });
 }
 
 // ---- observations ---------------------------------------------------------------------------
@@ -1207,6 +1257,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
     constexpr bool KAR = !(FAM == 2 && R >= 17) && !(sizeof(RT) == 4 && R >= 32);
+    // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
+    // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
+    // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
+    constexpr int SPD = (MODE >= 1 && W == 4) ? 4 : 0;
     const KArgs& a_in = a;
     QC_STAMP_BEGIN();
     for (int k = 0; k < n_my; ++k) {
@@ -1365,7 +1419,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 }
             }
             QC_STAMP(7);
-            band_solve<KL, R, MODE, false, true, 64>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
+            band_solve<KL, R, MODE, false, true, 64, SPD>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
             QC_STAMP(8);
             {
                 // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
@@ -1560,7 +1614,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         }
         QC_STAMP(7);
         // implicit Crank-Nicolson solve (IHO:487)
-        band_solve<KL, R, MODE, FAM == 1, SYMT, LE>(acc, tb, kf, kb, lnv QC_SOLVE_STAMP_PASS);
+        band_solve<KL, R, MODE, FAM == 1, SYMT, LE, SPD>(acc, tb, kf, kb, lnv QC_SOLVE_STAMP_PASS);
         QC_STAMP(8);
         // normalise (IHO:216-220, QO:259-263) + next <x> + Fail (IHO:422-426, QO:559-565) + IQO window
         {

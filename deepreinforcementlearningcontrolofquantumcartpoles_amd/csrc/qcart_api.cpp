@@ -237,7 +237,8 @@ KArgs base_args(const qc_handle* h) {
         const size_t t1 = L.tf, t2 = L.tf + (size_t)(2 * NL + 2) * op.kl * op.kl * op.lanes * es;
         // fp64 Fock families append the slot's H_F force coefficients (R+1 doubles per lane), the grid its
         // row constants (H_F's folded diagonal and x_r: 2R doubles per lane, RowLds)
-        const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1) * kWave * 8)
+        // (IHO: and X^2's diagonal, R doubles per lane)
+        const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1 + (op.family == QC_IHO ? op.R : 0)) * kWave * 8)
                                   : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
         int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
@@ -265,6 +266,7 @@ KArgs base_args(const qc_handle* h) {
     a.c = op.c;
     a.h = op.fock ? 1.0 : op.h;
     const double dt = p.dt;
+    a.x2h = op.family == QC_IHO ? -1.0 / op.c : 0.0;
     a.a2 = dt * dt * dt / 12.;
     a.a3 = dt * dt * dt * dt / 24.;
     a.a4 = dt * dt * dt * dt * dt / 80.;

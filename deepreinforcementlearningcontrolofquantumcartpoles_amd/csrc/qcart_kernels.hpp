@@ -1180,6 +1180,15 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                     const double x = (r >= 0 && r < a.Npad) ? a.xu[r] : 0.0;
                     *(double*)(fimg + t * 512 + lane * 8) = -cFs * x;
                 }
+                if constexpr (FAM == 1) {   // X^2's diagonal X[r][r-1]^2 + X[r][r+1]^2 (X2H, below)
+#pragma unroll
+                    for (int t = 0; t < R; ++t) {
+                        const int r = lane * R + t;
+                        const double xl = (r >= 1 && r - 1 < a.Npad) ? a.xu[r - 1] : 0.0;
+                        const double xr = r < a.Npad ? a.xu[r] : 0.0;
+                        *(double*)(fimg + (R + 1 + t) * 512 + lane * 8) = xl * xl + xr * xr;
+                    }
+                }
             }
         }
         __syncthreads();
@@ -1262,6 +1271,14 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
     constexpr int SPD = (MODE >= 1 && W == 4) ? 4 : 0;
     const KArgs& a_in = a;
+    // lazy normalisation: psi (and the Fock X psi) are carried unnormalised from step to step — scl is the
+    // scale that normalises them, sq = scl^2 (1 before the first step: psi is loaded normalised). The scheme
+    // is linear in psi given its scalar means, and psi' /= |psi'| cancels any factor, so only the quadratic
+    // forms inside a step (the Y+- means, the Phi+- products) take sq; the 2 R (Fock: 4 R) scaling multiplies
+    // per step move to one pass after the loop. Not in the fp32 kernel (C5), where the loop-carried scale
+    // costs the R = 32 kernel spills
+    constexpr bool LAZY = sizeof(RT) == 8;
+    double scl = 1.0, sq = 1.0;
     QC_STAMP_BEGIN();
     for (int k = 0; k < n_my; ++k) {
         // KAR: the loop's uniform constants are re-read from the kernarg segment every step (s_load through
@@ -1379,8 +1396,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                     sm[1] += (double)(x * (Ym[j].re * Ym[j].re + Ym[j].im * Ym[j].im));
                 }
                 step_sum<2>(sm);
-                yp = a.w * sm[0];
-                ym = a.w * sm[1];
+                yp = (a.w * sq) * sm[0];
+                ym = (a.w * sq) * sm[1];
             }
             {
                 // Y- branch: acc -= (c1 - c6) (-i H_F Y-); acc += (kRe x + kDm) rel-, rel- = (x - ym) Y-
@@ -1408,7 +1425,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 step_sum<2>(d2);
                 QC_STAMP(6);
                 const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp, k5 = c5 * beta;
-                const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
+                const double wq = a.w * sq;
+                const double dpm = 2.0 * wq * kP * d2[0], spm = 2.0 * yp + 2.0 * wq * kP * kP * d2[1];
                 // acc += fx X rel+ + fy Y+ + fr rel+ = (fx x (x - yp) + fy + fr (x - yp)) Y+
                 const RT fx = (RT)(kRed + 2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(kDpd - k5 * kP * spm);
                 const auto rc2 = rowc();
@@ -1443,7 +1461,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
                 scale = scale * a.inv_sqrt_w;
 #pragma unroll
-                for (int j = 0; j < R; ++j) psi[j] = C(acc[j].re * (RT)scale, acc[j].im * (RT)scale);
+                for (int j = 0; j < R; ++j) psi[j] = acc[j];   // unnormalised (scl; the grid is fp64 only)
+                scl = scale;
+                sq = scale * scale;
                 xbar = (RT)(a.w * (s[1] * scale) * scale);
                 const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
                 const bool f = stop * sc2 > thr2 || sbot * sc2 > thr2;
@@ -1537,8 +1557,16 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         const RT kY = (RT)(HC ? a.k_sb : sdt * beta), kIm = (RT)(c1 - c6);
         const double kP = HC ? a.k_sb : sdt * beta;
         // Y+- = Y0 +- kY rel (Y+ in psi's registers) and their unnormalised means in one reduction
+        // X2H (IHO, fp64 tables in LDS): X^2 = al H + diag(d) on the truncated Fock operators (H = -w/2 (a^2 +
+        // a+^2), X = (a + a+)/sqrt2: X^2's +-2 bands are -H/w, its diagonal d_r = X[r][r-1]^2 + X[r][r+1]^2, both
+        // to rounding), so every X rel+- of the branches is al H Y+- + d Y+- - y+- X Y+-: H Y+- is computed for
+        // the branch anyway, and no X application of rel+- (nor its halo) remains. The Phi products follow from
+        // S1 = <Y+, X Y+>, S2 = |X Y+|^2, S3 = <X Y+, X^2 Y+>:  <Y+, X rel+> + <rel+, X Y+> = 2 (S2 - yp S1),
+        // <rel+, X rel+> = S3 - 2 yp S2 + yp^2 S1 (unnormalised sums; yp the true mean)
+        constexpr bool X2H = FAM == 1 && FXL && R <= 8;   // (R = 16, one wave per SIMD: +88 spilled registers)
+        auto xdiag = [&](int j) -> RT { return *(const RT*)(tb.lds + tb.vr + lds_fx + (R + 1 + j) * 64 * (int)sizeof(RT)); };
         cx<RT> xYp[R];
-        double yp, ym;
+        double yp, ym, s1p;
         {
             cx<RT> Ym[R], xYm[R];
 #pragma unroll
@@ -1556,9 +1584,22 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             }
             double sm[2] = {q0.sum(), q1.sum()};
             step_sum<2>(sm, lnv);
-            yp = a.w * sm[0];
-            ym = a.w * sm[1];
+            yp = (a.w * sq) * sm[0];
+            ym = (a.w * sq) * sm[1];
+            s1p = sm[0];
             const RT ymr = (RT)ym;
+            if constexpr (X2H) {
+                // acc -= (c1-c6) (-i H_F Y-) + kRe X rel- + kDm rel-, X rel- = al H Y- + d Y- - ym X Y-, rel- = X Y- - ym Y-:
+                //   acc += kRe al h + (kRe d - kDm ym) y + (kDm - kRe ym) x  and  -+ kIm (h - cF x) crossed (h = H Y-)
+                const double kRed = -(c2 - c1) * g4, kDmd = (c4 - c3 + c5) * beta - kRed * ym;
+                const RT kRe = (RT)kRed, kH = (RT)(kRed * a.x2h), kX = (RT)(kDmd - kRed * ym), nk = (RT)(-kDmd * ym),
+                         kIc = kIm * cF;
+                h_rows<FAM, R>(Ym, cf, lnv, [&](int j, RT hre, RT him) {
+                    const RT cy = kRe * xdiag(j) + nk;
+                    acc[j] = C(acc[j].re + kH * hre - kIm * him + cy * Ym[j].re + kX * xYm[j].re + kIc * xYm[j].im,
+                               acc[j].im + kH * him + kIm * hre + cy * Ym[j].im + kX * xYm[j].im - kIc * xYm[j].re);
+                });
+            } else {
             // Y- branch: acc -= (c1-c6) (-i H_F Y-), fused row by row with H Y- (no H Y- vector)
             {
                 h_rows<FAM, R>(Ym, cf, lnv, [&](int j, RT hre, RT him) {
@@ -1575,9 +1616,37 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 acc[j] = C(acc[j].re + kRe * Ym[j].re + kDm * xYm[j].re, acc[j].im + kRe * Ym[j].im + kDm * xYm[j].im);
+            }
         }
         QC_STAMP(4);
-        {
+        if constexpr (X2H) {
+            // Y+ branch: +(c1-c6) (-i H_F Y+) row by row with t = X^2 Y+ = al H Y+ + d Y+ (kept; X rel+ = t - yp X Y+)
+            // and the lane's S2, S3
+            cx<RT> t[R];
+            const RT al = (RT)a.x2h, kIc = kIm * cF;
+            RowDot<RT> q2, q3;
+            h_rows<FAM, R>(psi, cf, lnv, [&](int j, RT hre, RT him) {
+                acc[j] = C(acc[j].re + kIm * him - kIc * xYp[j].im, acc[j].im - kIm * hre + kIc * xYp[j].re);
+                const RT dj = xdiag(j);
+                t[j] = C(al * hre + dj * psi[j].re, al * him + dj * psi[j].im);
+                q2.add(j == 0, xYp[j], xYp[j]);
+                q3.add(j == 0, xYp[j], t[j]);
+            });
+            double d2[2] = {q2.sum(), q3.sum()};
+            step_sum<2>(d2, lnv);
+            QC_STAMP(6);
+            const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp, k5 = c5 * beta;
+            const double wq = a.w * sq;
+            const double p0 = 2.0 * (d2[0] - yp * s1p), p1 = d2[1] - 2.0 * yp * d2[0] + yp * yp * s1p;
+            const double dpm = 2.0 * wq * kP * p0, spm = 2.0 * yp + 2.0 * wq * kP * kP * p1;
+            // acc += fx X rel+ + fy Y+ + fr rel+ = fx t + (fy - fr yp) Y+ + (fr - fx yp) X Y+
+            const double fxd = kRed + 2.0 * k5 * kP, frd = kDpd - k5 * kP * spm, fyd = -k5 * dpm;
+            const RT fx = (RT)fxd, fy = (RT)(fyd - frd * yp), fr = (RT)(frd - fxd * yp);
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                acc[j] = C(acc[j].re + fx * t[j].re + fy * psi[j].re + fr * xYp[j].re,
+                           acc[j].im + fx * t[j].im + fy * psi[j].im + fr * xYp[j].im);
+        } else {
             // Y+ branch (Y+ in psi); keeps X Y+, rel+ and X rel+ for the Phi means
             cx<RT> rp[R], xrp[R];
             const RT ypr = (RT)yp;
@@ -1604,7 +1673,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             QC_STAMP(6);
             // (X Phi+ - pp Phi+) - (X Phi- - pm Phi-) = 2 kP X rel+ - (pp - pm) Y+ - kP (pp + pm) rel+
             const double k5 = c5 * beta;
-            const double dpm = 2.0 * a.w * kP * d2[0], spm = 2.0 * yp + 2.0 * a.w * kP * kP * d2[1];
+            const double wq = a.w * sq;
+            const double dpm = 2.0 * wq * kP * d2[0], spm = 2.0 * yp + 2.0 * wq * kP * kP * d2[1];
             // with this branch's kRe X rel+ + kDp rel+ folded in (one pass over acc)
             const RT fx = (RT)(kRed + 2.0 * k5 * kP), fy = (RT)(-k5 * dpm), fr = (RT)(kDpd - k5 * kP * spm);
 #pragma unroll
@@ -1662,9 +1732,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
             if constexpr (FAM == 2) scale = scale * a.inv_sqrt_w;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-                psi[j] = C(acc[j].re * (RT)scale, acc[j].im * (RT)scale);
-                xp[j] = C(xn[j].re * (RT)scale, xn[j].im * (RT)scale);
+            for (int j = 0; j < R; ++j) {   // LAZY: unnormalised (scl)
+                psi[j] = LAZY ? acc[j] : C(acc[j].re * (RT)scale, acc[j].im * (RT)scale);
+                xp[j] = LAZY ? xn[j] : C(xn[j].re * (RT)scale, xn[j].im * (RT)scale);
+            }
+            if constexpr (LAZY) {
+                scl = scale;
+                sq = scale * scale;
             }
             xbar = (RT)(a.w * (s[1] * scale) * scale);
             // check_boundary_error: sqrt(sum |psi|^2) > thr, compared squared (no square roots)
@@ -1683,6 +1757,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         }   // Fock families
     }
     QC_STAMP_END(lane);
+    if constexpr (LAZY) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) psi[j] = C(psi[j].re * (RT)scl, psi[j].im * (RT)scl);   // normalised
+    }
     if constexpr (RCL) load_coef<FAM, R>(cf, a, base);   // x_r for grid_obs (not held across the loop)
     // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
     // across the loop)
@@ -2015,7 +2093,7 @@ static inline unsigned nblocks(int64_t B) { return (unsigned)((B + 3) / 4); }
 template <int FAM, int R, typename RT>
 constexpr uint32_t kDualImg =
     slot_layout(Fam<FAM>::KL, R, FAM == 1, (uint32_t)sizeof(cx<RT>), slot_sym(FAM != 2, (uint32_t)sizeof(cx<RT>), 64), 64).tf +
-    (FAM <= 1 ? (uint32_t)(R + 1) * 64u * 8u : 0u);
+    (FAM <= 1 ? (uint32_t)(R + 1 + (FAM == 1 ? R : 0)) * 64u * 8u : 0u);
 template <int FAM, int R, typename RT>
 constexpr bool kDual = sizeof(RT) == 8 && !(FAM == 2 && grid_rows_in_lds(R)) && 2u * ((kDualImg<FAM, R, RT> + 15u) & ~15u) <= 160u * 1024u;
 

@@ -99,6 +99,22 @@ __device__ __forceinline__ cx<RT> cmsub(cx<RT> acc, cx<RT> a, cx<RT> b) {
 }
 template <typename RT>
 __device__ __forceinline__ cx<RT> ld(const RT* p, size_t i) { return C(p[2 * i], p[2 * i + 1]); }
+// one complex element as a single vector access (p: its real part; complex arrays are element-aligned)
+template <typename RT>
+__device__ __forceinline__ cx<RT> ld_cx(const RT* p) {
+    if constexpr (sizeof(RT) == 8) {
+        const double2 v = *(const double2*)p;
+        return C(v.x, v.y);
+    } else {
+        const float2 v = *(const float2*)p;
+        return C(v.x, v.y);
+    }
+}
+template <typename RT>
+__device__ __forceinline__ void st_cx(RT* p, cx<RT> v) {
+    if constexpr (sizeof(RT) == 8) *(double2*)p = make_double2(v.re, v.im);
+    else *(float2*)p = make_float2(v.re, v.im);
+}
 // s + Re<a, b> for one row of a lane-partial sum: fp64 as one FMA chain (the first row starts the
 // chain: no "+ 0"), fp32 products summed in fp32 and accumulated in fp64
 template <typename RT>
@@ -997,10 +1013,53 @@ __device__ __forceinline__ void grid_p(const cd (&v)[R], cd (&o)[R], double pbar
 constexpr int kMaxMoment = 6;                 // obs vector up to (2+6+1)*6/2 = 27
 constexpr int kMaxObs = (2 + kMaxMoment + 1) * kMaxMoment / 2;
 
-// compute_statistics (QO/simulation_quart.cpp:326-362)
+// compute_statistics (QO/simulation_quart.cpp:326-362). Returns this lane's entry of the observation vector
+// (lane 0 <x>, lane 1 <p>, lane i >= 2 the centred moment i; lanes >= n_obs: unused): the moments of one p-power b
+// are summed over the wave as soon as they are complete, so no lane holds the whole 27-entry vector (holding it
+// across the p-power passes spilled the R = 17 step kernel's epilogue: 804 B of scratch per lane, written back
+// once per wave — ~0.8 GB per C3 launch)
+// the moments x^aa p^B (2 <= aa + B <= kMaxMoment) of one p-power B, then B + 1 (v: p^(B-1) psi on entry).
+// PS(j): psi's row j. (Measured and not kept: at R = 17 a re-read of the env's just-written rows from HBM instead of
+// psi's registers — the scheduler batches the re-reads, 156 -> 216 spilled registers)
+template <int B, int R, typename PS>
+__device__ __forceinline__ void grid_obs_pow(const PS& ps, cd (&v)[R], const Coef<2, R>& cf, int lane, int m,
+                                             double xbar, double pbar, double inv_h, double h, double& ov) {
+    if constexpr (B <= kMaxMoment) {
+        if (B > m) return;
+        if constexpr (B > 0) {
+            cd nv[R];
+            grid_p<R>(v, nv, pbar, inv_h, cf.N, cf.base, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = nv[j];
+        }
+        constexpr int A0 = B >= 2 ? 0 : 2 - B, A1 = kMaxMoment - B, NA = A1 - A0 + 1;
+        double acc[NA];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double xr = cf.xg[j] - xbar;
+            const cd pj = ps(j);
+            const double base_re = pj.re * v[j].re + pj.im * v[j].im;   // Re conj(psi) v
+            double xa = 1.0;
+#pragma unroll
+            for (int aa = 0; aa <= A1; ++aa) {
+                if (aa >= A0) acc[aa - A0] += xa * base_re;
+                xa *= xr;
+            }
+        }
+        wave_sum<NA>(acc);
+#pragma unroll
+        for (int aa = A0; aa <= A1; ++aa) {
+            const int jj = aa + B, idx = 2 + (jj - 2) * (jj + 3) / 2 + B;
+            ov = lane == idx ? acc[aa - A0] * h : ov;
+        }
+        grid_obs_pow<B + 1, R>(ps, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+    }
+}
+
 template <int R>
-__device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, int lane, int m, double h,
-                                         double (&o)[kMaxObs]) {
+__device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, int lane, int m, double h) {
     const double inv_h = 1.0 / h;
     cd v[R];
     double s2[2] = {0, 0};
@@ -1012,41 +1071,12 @@ __device__ __forceinline__ void grid_obs(const cd (&psi)[R], const Coef<2, R>& c
     }
     wave_sum<2>(s2);
     const double xbar = s2[0] * h, pbar = s2[1] * h;
-    double acc[kMaxObs];
-#pragma unroll
-    for (int i = 0; i < kMaxObs; ++i) acc[i] = 0.0;
+    double ov = lane == 0 ? xbar : pbar;
 #pragma unroll
     for (int j = 0; j < R; ++j) v[j] = psi[j];
-#pragma unroll
-    for (int b = 0; b <= kMaxMoment; ++b) {
-        if (b > m) break;
-        if (b > 0) {
-            cd nv[R];
-            grid_p<R>(v, nv, pbar, inv_h, cf.N, cf.base, lane);
-#pragma unroll
-            for (int j = 0; j < R; ++j) v[j] = nv[j];
-        }
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const double xr = cf.xg[j] - xbar;
-            const double base_re = psi[j].re * v[j].re + psi[j].im * v[j].im;   // Re conj(psi) v
-            double xa = 1.0;
-#pragma unroll
-            for (int aa = 0; aa <= kMaxMoment; ++aa) {
-                const int jj = aa + b;
-                if (jj >= 2 && jj <= kMaxMoment) {
-                    const int idx = 2 + (jj - 2) * (jj + 3) / 2 + b;
-                    acc[idx] += xa * base_re;
-                }
-                xa *= xr;
-            }
-        }
-    }
-    wave_sum<kMaxObs>(acc);
-    o[0] = xbar;
-    o[1] = pbar;
-#pragma unroll
-    for (int i = 2; i < kMaxObs; ++i) o[i] = acc[i] * h;
+    auto ps = [&](int j) -> cd { return psi[j]; };
+    grid_obs_pow<0, R>(ps, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+    return ov;
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
@@ -1202,13 +1232,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
 
     RT* gpsi = (RT*)a.psi + (size_t)env * N * 2;
     cx<RT> psi[R];
+    // psi: one whole-complex (16 B fp64 / 8 B fp32) access per row and lane; a wave's R accesses of a row index
+    // cover its env's lines completely, so the L2 hands HBM whole lines. (Non-temporal 8-B accesses of the real
+    // and imaginary halves, round 3's first variant, reached HBM as partial writes: 2.2 GB written per metric
+    // launch for 0.54 GB of psi, 4.7 GB at C5, and 1.8x the read bytes)
 #pragma unroll
-    // psi streams through once per launch: non-temporal loads and stores, so it does not evict what the L2
-    // should keep (the slot tables, and the scratch lines of the kernels that spill)
     for (int j = 0; j < R; ++j)
-        psi[j] = (base + j < N) ? C(__builtin_nontemporal_load(gpsi + 2 * (base + j)),
-                                    __builtin_nontemporal_load(gpsi + 2 * (base + j) + 1))
-                                : C(RT(0), RT(0));
+        psi[j] = (base + j < N) ? ld_cx<RT>(gpsi + 2 * (base + j)) : C(RT(0), RT(0));
 
     const bool win_on = a.win_hi > a.win_lo;
     // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)
@@ -1769,10 +1799,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         asm volatile("" : "+v"(wb));
 #pragma unroll
         for (int j = 0; j < R; ++j)
-            if (wb + j < N) {
-                __builtin_nontemporal_store(psi[j].re, gpsi + 2 * (wb + j));
-                __builtin_nontemporal_store(psi[j].im, gpsi + 2 * (wb + j) + 1);
-            }
+            if (wb + j < N) st_cx<RT>(gpsi + 2 * (wb + j), psi[j]);
     }
     if (lane == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
@@ -1790,14 +1817,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 a.obs_out[(size_t)env * 5 + lane] = v;
             }
         } else {
-            double o[kMaxObs];
-            grid_obs<R>(psi, cf, lane, a.moment_order, a.h, o);
-            if (lane < a.n_obs) {
-                double v = o[0];
-#pragma unroll
-                for (int i = 1; i < kMaxObs; ++i) v = (lane == i) ? o[i] : v;
-                a.obs_out[(size_t)env * a.n_obs + lane] = v;
-            }
+            const double v = grid_obs<R>(psi, cf, lane, a.moment_order, a.h);
+            if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
         }
     }
     QC_KSTAMP_EXIT(lane);
@@ -1855,14 +1876,8 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
             a.obs_out[(size_t)env * 5 + lane] = v;
         }
     } else {
-        double o[kMaxObs];
-        grid_obs<R>(psi, cf, lane, a.moment_order, a.h, o);
-        if (lane < a.n_obs) {
-            double v = o[0];
-#pragma unroll
-            for (int i = 1; i < kMaxObs; ++i) v = (lane == i) ? o[i] : v;
-            a.obs_out[(size_t)env * a.n_obs + lane] = v;
-        }
+        const double v = grid_obs<R>(psi, cf, lane, a.moment_order, a.h);
+        if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
     }
 }
 

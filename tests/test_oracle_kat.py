@@ -217,3 +217,36 @@ def test_outside_probability_window(oracle_mod):
     ref = 1.0 - np.sum(np.abs(psi[c - w:c + w]) ** 2) * 0.05
     assert abs(s.outside_prob(psi, xth) - ref) < 1e-15
     assert abs(xth - 5.0) < 1e-12
+
+
+# ---- the IHO step kernel's X^2 identity (k_step X2H) ----------------------------
+@pytest.mark.parametrize("n_max,omega", [(511, pi), (180, pi), (40, 2.0)])
+def test_iho_x_squared_is_h_multiple_plus_diagonal(n_max, omega):
+    """On the truncated Fock operators of IHO/simulation_i.cpp:65-124, X^2 = -H/omega + diag(d) with
+    d_r = X[r][r-1]^2 + X[r][r+1]^2 (the truncation's last row included) — to rounding."""
+    ops = R.fock_ops(n_max, omega, inverted=True)
+    x, H = ops["x"], ops["H"]
+    xu = np.diag(x, 1)
+    d = np.concatenate([[0.0], xu ** 2]) + np.concatenate([xu ** 2, [0.0]])
+    lhs = x @ x
+    rhs = -H / omega + np.diag(d)
+    assert np.max(np.abs(lhs - rhs)) <= 1e-15 * np.max(np.abs(lhs))
+
+
+def test_phi_products_from_s1_s2_s3():
+    """k_step's Y+ branch (X2H): with rel = X Y - m Y, the Phi products follow from S1 = <Y, XY>,
+    S2 = |XY|^2, S3 = <XY, X^2 Y>: <Y, X rel> + <rel, XY> = 2 (S2 - m S1), <rel, X rel> = S3 - 2 m S2 + m^2 S1;
+    and X rel = X^2 Y - m XY (IHO/simulation_i.cpp:301-333 computes X rel directly)."""
+    rng = np.random.default_rng(5)
+    ops = R.fock_ops(60, pi, inverted=True)
+    x = ops["x"]
+    y = rng.normal(size=61) + 1j * rng.normal(size=61)
+    y /= np.linalg.norm(y)
+    xy = x @ y
+    m = np.vdot(y, xy).real
+    rel = xy - m * y
+    s1, s2, s3 = np.vdot(y, xy).real, np.vdot(xy, xy).real, np.vdot(xy, x @ xy).real
+    direct0 = np.vdot(y, x @ rel).real + np.vdot(rel, xy).real
+    direct1 = np.vdot(rel, x @ rel).real
+    assert abs(direct0 - 2 * (s2 - m * s1)) < 1e-13
+    assert abs(direct1 - (s3 - 2 * m * s2 + m * m * s1)) < 1e-13

@@ -1021,9 +1021,11 @@ constexpr int kMaxObs = (2 + kMaxMoment + 1) * kMaxMoment / 2;
 // the moments x^aa p^B (2 <= aa + B <= kMaxMoment) of one p-power B, then B + 1 (v: p^(B-1) psi on entry).
 // PS(j): psi's row j. (Measured and not kept: at R = 17 a re-read of the env's just-written rows from HBM instead of
 // psi's registers — the scheduler batches the re-reads, 156 -> 216 spilled registers)
-template <int B, int R, typename PS>
-__device__ __forceinline__ void grid_obs_pow(const PS& ps, cd (&v)[R], const Coef<2, R>& cf, int lane, int m,
-                                             double xbar, double pbar, double inv_h, double h, double& ov) {
+// XM(): an accessor of the rows' x_r (.x(j)) — cf.xg, or (R = 17 step kernel) the block's LDS row constants, made
+// fresh per pass so that the 2 R registers of x are not held across the passes
+template <int B, int R, typename PS, typename XM>
+__device__ __forceinline__ void grid_obs_pow(const PS& ps, const XM& xm, cd (&v)[R], const Coef<2, R>& cf, int lane,
+                                             int m, double xbar, double pbar, double inv_h, double h, double& ov) {
     if constexpr (B <= kMaxMoment) {
         if (B > m) return;
         if constexpr (B > 0) {
@@ -1036,9 +1038,10 @@ __device__ __forceinline__ void grid_obs_pow(const PS& ps, cd (&v)[R], const Coe
         double acc[NA];
 #pragma unroll
         for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+        const auto xs = xm();
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const double xr = cf.xg[j] - xbar;
+            const double xr = xs.x(j) - xbar;
             const cd pj = ps(j);
             const double base_re = pj.re * v[j].re + pj.im * v[j].im;   // Re conj(psi) v
             double xa = 1.0;
@@ -1054,19 +1057,21 @@ __device__ __forceinline__ void grid_obs_pow(const PS& ps, cd (&v)[R], const Coe
             const int jj = aa + B, idx = 2 + (jj - 2) * (jj + 3) / 2 + B;
             ov = lane == idx ? acc[aa - A0] * h : ov;
         }
-        grid_obs_pow<B + 1, R>(ps, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+        grid_obs_pow<B + 1, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
     }
 }
 
-template <int R>
-__device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, int lane, int m, double h) {
+template <int R, typename XM>
+__device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, const XM& xm, int lane, int m,
+                                           double h) {
     const double inv_h = 1.0 / h;
     cd v[R];
     double s2[2] = {0, 0};
     grid_p<R>(psi, v, 0.0, inv_h, cf.N, cf.base, lane);
+    const auto xs = xm();
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        s2[0] += cf.xg[j] * (psi[j].re * psi[j].re + psi[j].im * psi[j].im);
+        s2[0] += xs.x(j) * (psi[j].re * psi[j].re + psi[j].im * psi[j].im);
         s2[1] += psi[j].re * v[j].re + psi[j].im * v[j].im;
     }
     wave_sum<2>(s2);
@@ -1075,7 +1080,7 @@ __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>&
 #pragma unroll
     for (int j = 0; j < R; ++j) v[j] = psi[j];
     auto ps = [&](int j) -> cd { return psi[j]; };
-    grid_obs_pow<0, R>(ps, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+    grid_obs_pow<0, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
     return ov;
 }
 
@@ -1791,7 +1796,6 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
 #pragma unroll
         for (int j = 0; j < R; ++j) psi[j] = C(psi[j].re * (RT)scl, psi[j].im * (RT)scl);   // normalised
     }
-    if constexpr (RCL) load_coef<FAM, R>(cf, a, base);   // x_r for grid_obs (not held across the loop)
     // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
     // across the loop)
     {
@@ -1817,7 +1821,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 a.obs_out[(size_t)env * 5 + lane] = v;
             }
         } else {
-            const double v = grid_obs<R>(psi, cf, lane, a.moment_order, a.h);
+            const double v = grid_obs<R>(psi, cf, rowc, lane, a.moment_order, a.h);
             if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
         }
     }
@@ -1876,7 +1880,8 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
             a.obs_out[(size_t)env * 5 + lane] = v;
         }
     } else {
-        const double v = grid_obs<R>(psi, cf, lane, a.moment_order, a.h);
+        auto xm = [&]() { return RowReg<R>{cf.xg, cf.xg}; };
+        const double v = grid_obs<R>(psi, cf, xm, lane, a.moment_order, a.h);
         if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
     }
 }

@@ -240,10 +240,16 @@ KArgs base_args(const qc_handle* h) {
         // (IHO: and X^2's diagonal, R doubles per lane)
         const size_t fx = op.fock ? (f32 ? 0 : (size_t)(op.R + 1 + (op.family == QC_IHO ? op.R : 0)) * kWave * 8)
                                   : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
-        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : (t1 + fx <= 160 * 1024 ? 1 : 0);
-        if (const char* e = std::getenv("QCART_TAB_MODE")) mode = std::min(mode, std::atoi(e));
+        // MODE 4 (grid R >= 17): the forward levels + prefix only, beside the row constants
+        const size_t t4 = L.tf + (size_t)(NL + 1) * op.kl * op.kl * op.lanes * es;
+        const bool m4 = !op.fock && !f32 && grid_rows_in_lds(op.R) && lf <= NL && t4 + fx <= 160 * 1024;
+        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : m4 ? 4 : (t1 + fx <= 160 * 1024 ? 1 : 0);
+        if (const char* e = std::getenv("QCART_TAB_MODE")) {   // a cap: 0 < 1 < 4 < 2 in LDS use
+            const int c = std::atoi(e);
+            if (mode != 4 || c < 2) mode = std::min(mode, c);
+        }
         a.tab_mode = mode;
-        a.lds_fx = (uint32_t)(mode == 2 ? t2 : t1);
+        a.lds_fx = (uint32_t)(mode == 2 ? t2 : mode == 4 ? t4 : t1);
         a.lds_bytes = mode ? (uint32_t)(a.lds_fx + fx) : 0u;
         // two-slot blocks (MODE 3) share the launch: the dynamic LDS covers two slot images
         if (h->dual_img && mode >= 1) {

@@ -74,7 +74,7 @@ struct KArgs {
     int32_t moment_order;
     int32_t n_obs;
     int32_t precision;         // 0 fp64, 1 fp32 (psi storage and step arithmetic)
-    int32_t tab_mode;          // step kernel factor tables: 0 global, 1 LDS (lc/uc/di/m2), 2 + composites
+    int32_t tab_mode;          // step kernel factor tables: 0 global, 1 LDS (lc/uc/di/m2), 2 + composites, 4 + forward composites
     uint32_t lds_bytes;        // dynamic LDS per block for tab_mode >= 1
     uint32_t lds_fx;           // LDS offset of the H_F force coefficients (Fock, tab_mode >= 1)
     const int32_t* order;      // [n_blocks*W] envs grouped by force slot (-1 idle) or null (identity)

@@ -708,8 +708,12 @@ struct Tab {
         if constexpr (MODE >= 1) return *(const RT*)atr(off);
         else return bld_d<RT>(rs, vr, (int)off);
     }
-    __device__ __forceinline__ cx<RT> comp(uint32_t off) const {   // scan composites
+    __device__ __forceinline__ cx<RT> comp(uint32_t off) const {   // backward scan composites
         if constexpr (MODE == 2) return lds_c(atc(off));
+        else return bld_c<RT>(rs, vc, (int)off);
+    }
+    __device__ __forceinline__ cx<RT> compf(uint32_t off) const {  // forward scan composites (MODE 4: LDS too)
+        if constexpr (MODE == 2 || MODE == 4) return lds_c(atc(off));
         else return bld_c<RT>(rs, vc, (int)off);
     }
 };
@@ -737,7 +741,8 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
         if (lvl < nlev) {
             cx<RT> T[KL * KL];
 #pragma unroll
-            for (int e = 0; e < KL * KL; ++e) T[e] = tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * CE);
+            for (int e = 0; e < KL * KL; ++e)
+                T[e] = FWD ? tb.compf(lv0 + (uint32_t)(lvl * KL * KL + e) * CE) : tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * CE);
             cx<RT> p[KL];
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
@@ -755,7 +760,7 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
     }
     cx<RT> P[KL * KL];
 #pragma unroll
-    for (int e = 0; e < KL * KL; ++e) P[e] = tb.comp(lvp + (uint32_t)e * CE);
+    for (int e = 0; e < KL * KL; ++e) P[e] = FWD ? tb.compf(lvp + (uint32_t)e * CE) : tb.comp(lvp + (uint32_t)e * CE);
     cx<RT> c[KL];
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
@@ -817,7 +822,8 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
     // MODE 2 image (fixed, compile-time offsets): forward levels 0..NL-1, forward P, backward 0..NL-1,
     // backward P (the host uses MODE 2 only when every slot keeps <= NL levels per direction)
     constexpr uint32_t NL = (uint32_t)mode2_levels(KL);
-    constexpr uint32_t f0 = SL.tf, fP = MODE == 2 ? SL.tf + NL * CB : SL.tf + 6u * CB;
+    // MODE 4: the forward levels + prefix in LDS (as MODE 2), the backward ones from the global block (as MODE 1)
+    constexpr uint32_t f0 = SL.tf, fP = (MODE == 2 || MODE == 4) ? SL.tf + NL * CB : SL.tf + 6u * CB;
     constexpr uint32_t b0 = MODE == 2 ? SL.tf + (NL + 1u) * CB : SL.tb;
     constexpr uint32_t bP = MODE == 2 ? SL.tf + (2u * NL + 1u) * CB : SL.tb + 6u * CB;
     // backward factor k of row j (k = 0..KL-1 multiplies x_{j+1+k})
@@ -829,7 +835,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
             return t.c(SL.uc + (uint32_t)(k * R + j) * CE);
         }
     };
-    const bool hf = MODE == 2 || kf <= 4, hb = MODE == 2 || kb <= 4;
+    const bool hf = MODE == 2 || MODE == 4 || kf <= 4, hb = MODE == 2 || kb <= 4;
     // forward, pass 1 (zero incoming state): lane end state e_l
     cx<RT> s[KL];
 #pragma unroll
@@ -867,7 +873,7 @@ __device__ __forceinline__ void band_solve(cx<RT> (&b)[R], const Tab<MODE, RT>& 
                 for (int i = 0; i < KL; ++i)
 #pragma unroll
                     for (int k = 0; k < KL; ++k)
-                        s[i] = cmac(s[i], tb.comp(f0 + (uint32_t)(lvl * KL * KL + i * KL + k) * CE), p[k]);
+                        s[i] = cmac(s[i], tb.compf(f0 + (uint32_t)(lvl * KL * KL + i * KL + k) * CE), p[k]);
             }
         }
     }
@@ -1187,12 +1193,14 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         } else {
             copy(0, 0, SL.tf);
         }
-        if constexpr (MODE == 2) {   // the kept composite levels at their fixed places (band_solve)
+        if constexpr (MODE == 2 || MODE == 4) {   // the kept composite levels at their fixed places (band_solve)
             constexpr uint32_t CB = KL * KL * CE, NL = (uint32_t)mode2_levels(KL);
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
             copy(SL.tf + 6u * CB, SL.tf + NL * CB, CB);
-            copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
-            copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
+            if constexpr (MODE == 2) {
+                copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
+                copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
+            }
         }
         static_assert(!(FAM == 2 && MODE == 3 && grid_rows_in_lds(R)), "two-slot blocks carry no row constants");
         if constexpr (FAM == 2 && MODE >= 1 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x
@@ -2117,6 +2125,11 @@ constexpr uint32_t kDualImg =
 template <int FAM, int R, typename RT>
 constexpr bool kDual = sizeof(RT) == 8 && !(FAM == 2 && grid_rows_in_lds(R)) && 2u * ((kDualImg<FAM, R, RT> + 15u) & ~15u) <= 160u * 1024u;
 
+// MODE 4 (the tables + the forward scan composites in LDS, the backward composites from L2) is instantiated for
+// the kernels whose MODE 2 image does not fit beside the grid row constants: the R = 17 grid kernel (C3)
+template <int FAM, int R>
+constexpr bool kMode4 = FAM == 2 && grid_rows_in_lds(R);
+
 template <int FAM, int R, int MODE, typename RT, bool DUAL = false>
 int launch_step_mode(const KArgs& a, hipStream_t st) {
     const dim3 grid(a.n_blocks + (DUAL ? a.n_mixed : 0u)), block(64 * kStepWaves<FAM, R, RT>);
@@ -2148,6 +2161,13 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
             if (a.n_mixed > 0 && a.tab_mode >= 1) {
                 rc = a.tab_mode == 2 ? launch_step_mode<FAM, R, 2, RT, true>(a, st)
                                      : launch_step_mode<FAM, R, 1, RT, true>(a, st);
+                if (rc) return rc;
+                return hipGetLastError() == hipSuccess ? 0 : -3;
+            }
+        }
+        if constexpr (kMode4<FAM, R>) {
+            if (a.tab_mode == 4) {
+                rc = launch_step_mode<FAM, R, 4, RT>(a, st);
                 if (rc) return rc;
                 return hipGetLastError() == hipSuccess ? 0 : -3;
             }

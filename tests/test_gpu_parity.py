@@ -386,12 +386,12 @@ def test_empty_inputs_and_single_env(oracle_mod, name):
     assert float(wnorm(ph, psi.cpu().numpy() - ref)[0]) < 1e-10
 
 
-@pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513"])
+@pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513", "qo1025"])
 def test_table_placements_bitwise_equal(monkeypatch, case):
     """The step kernel's factor-table placements (0: global buffer loads, 1: workgroup LDS image of
-    lc/uc/di/m2, 2: + scan composites) agree (1 and 2 bit-identical; 0 may contract differently,
-    <1e-12), with envs of mixed force slots grouped per workgroup; the grouping must not change any
-    env's trajectory (bitwise)."""
+    lc/uc/di/m2, 2: + scan composites; qo1025 (C3): 4 — the forward composites only — in place of 2) agree
+    (1 and 2 / 4 bit-identical; 0 may contract differently, <1e-12), with envs of mixed force slots grouped per
+    workgroup; the grouping must not change any env's trajectory (bitwise)."""
     ph = CASES[case]
     B = 37
     st = Stepper(ph, B, 0, seed=11)

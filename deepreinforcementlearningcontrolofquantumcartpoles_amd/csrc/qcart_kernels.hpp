@@ -1091,9 +1091,12 @@ __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>&
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
-// waves (envs) per step workgroup: 8 (two per SIMD) where the step fits 256 VGPRs, else 4
+// waves (envs) per step workgroup: 8 (two per SIMD) where the step fits 256 VGPRs, else 4. The grid's R = 9
+// kernel (C4) runs two waves per SIMD although its loop then keeps ~16 scratch accesses per step: 10.8 -> 10.2 ms
+// at 8 192 envs, 82.1 -> 76.2 ms at 65 536 (same call; with two-slot workgroups no round is padded — in round 2,
+// with per-slot padding, it lost at 8 192)
 #ifndef QCART_W8_MAX_RG
-#define QCART_W8_MAX_RG 5
+#define QCART_W8_MAX_RG 9
 #endif
 #ifndef QCART_W8_MAX_R
 #define QCART_W8_MAX_R 8

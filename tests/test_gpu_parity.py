@@ -47,6 +47,8 @@ def wnorm(ph, v):
 CASES = {
     "iho64": cfg.DEFAULTS[cfg.IHO].with_(n_max=63),
     "iho181": cfg.DEFAULTS[cfg.IHO],
+    # omega != pi: the step kernel's X rel+- through X^2 = -H/omega + diag(d) at another omega
+    "iho181_w2": cfg.DEFAULTS[cfg.IHO].with_(omega=2.0),
     "iho512": cfg.DEFAULTS[cfg.IHO].with_(n_max=511),
     # gamma = 2 pi at N = 512 needs dt = 1/2880 for 1000 physical steps: at 1/1440 rounding in the top
     # Fock levels grows until the run blows up after ~700 steps (oracle and MKL-ordered stepper alike;
@@ -130,7 +132,8 @@ def run_pair(oracle_mod, ph, steps, B, act_lo, act_hi, chunk=80, seed=7, policy=
 
 
 @pytest.mark.parametrize("name,steps,B,policy", [
-    ("iho64", 1000, 8, "pd"), ("iho181", 1000, 8, "random"), ("iho512_g05", 1000, 8, "pd"),
+    ("iho64", 1000, 8, "pd"), ("iho181", 1000, 8, "random"), ("iho181_w2", 1000, 8, "random"),
+    ("iho512_g05", 1000, 8, "pd"),
     ("iho512_dt2", 1000, 8, "pd"), ("iho512_exact_g05", 1000, 4, "pd"),
     ("ho256", 1000, 6, "random"), ("ho71", 1000, 8, "random"), ("qo171", 1000, 6, "random"),
     ("iqo513", 1000, 4, "random"), ("qo1025", 1000, 3, "random"), ("iho1024_g05", 1000, 4, "pd"),

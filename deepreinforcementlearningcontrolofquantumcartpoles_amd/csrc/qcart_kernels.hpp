@@ -1609,8 +1609,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         // the branch anyway, and no X application of rel+- (nor its halo) remains. The Phi products follow from
         // S1 = <Y+, X Y+>, S2 = |X Y+|^2, S3 = <X Y+, X^2 Y+>:  <Y+, X rel+> + <rel+, X Y+> = 2 (S2 - yp S1),
         // <rel+, X rel+> = S3 - 2 yp S2 + yp^2 S1 (unnormalised sums; yp the true mean)
-        constexpr bool X2H = FAM == 1 && FXL && R <= 8;   // (R = 16, one wave per SIMD: +88 spilled registers)
-        auto xdiag = [&](int j) -> RT { return *(const RT*)(tb.lds + tb.vr + lds_fx + (R + 1 + j) * 64 * (int)sizeof(RT)); };
+        // (fp64 R = 16, one wave per SIMD: +88 spilled registers; fp32: d from the X rows in registers, its LDS
+        // image is full)
+        constexpr bool X2H = FAM == 1 && ((FXL && R <= 8) || sizeof(RT) == 4);
+        auto xdiag = [&](int j) -> RT {
+            if constexpr (FXL) return *(const RT*)(tb.lds + tb.vr + lds_fx + (R + 1 + j) * 64 * (int)sizeof(RT));
+            else return cf.xu[j] * cf.xu[j] + cf.xu[j + 1] * cf.xu[j + 1];
+        };
         cx<RT> xYp[R];
         double yp, ym, s1p;
         {

@@ -1446,28 +1446,40 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 ym = (a.w * sq) * sm[1];
             }
             {
-                // Y- branch: acc -= (c1 - c6) (-i H_F Y-); acc += (kRe x + kDm) rel-, rel- = (x - ym) Y-
+                // the branches' (c1 - c6) (-i H_F Y+) - (c1 - c6) (-i H_F Y-): H_F is linear, so one stencil
+                // application to Y+ - Y- instead of one per branch (on the grid H_F Y+- is needed for nothing else)
+                cx<RT> dv[R];
+#pragma unroll
+                for (int j = 0; j < R; ++j) dv[j] = C(psi[j].re - Ym[j].re, psi[j].im - Ym[j].im);
+                const auto rc = rowc();
+                grid_hf_rows<R>(dv, rc, cf, lane, [&](int j, RT hre, RT him) {
+                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);
+                });
+            }
+            {
+                // Y- branch: acc += (kRe x + kDm) rel-, rel- = (x - ym) Y-
                 const double kRed = -(c2 - c1) * g4;
                 const RT kRe = (RT)kRed, kDm = (RT)((c4 - c3 + c5) * beta - kRed * ym), ymr = (RT)ym;
                 const auto rc = rowc();
-                grid_hf_rows<R>(Ym, rc, cf, lane, [&](int j, RT hre, RT him) {
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
                     const RT x = (RT)rc.x(j), cr = (kRe * x + kDm) * (x - ymr);
-                    acc[j] = C(acc[j].re - kIm * him + cr * Ym[j].re, acc[j].im + kIm * hre + cr * Ym[j].im);
-                });
+                    acc[j] = C(acc[j].re + cr * Ym[j].re, acc[j].im + cr * Ym[j].im);
+                }
             }
             QC_STAMP(4);
             {
-                // Y+ branch: acc += (c1 - c6) (-i H_F Y+); rel+ = (x - yp) Y+, and the Phi+- means from
+                // Y+ branch: rel+ = (x - yp) Y+, and the Phi+- means from
                 // <Y+, X rel+> + <rel+, X Y+> = 2 x (x - yp) |Y+|^2 and <rel+, X rel+> = x (x - yp)^2 |Y+|^2
                 const RT ypr = (RT)yp;
                 double d2[2] = {0.0, 0.0};
                 const auto rc = rowc();
-                grid_hf_rows<R>(psi, rc, cf, lane, [&](int j, RT hre, RT him) {
-                    acc[j] = C(acc[j].re + kIm * him, acc[j].im - kIm * hre);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
                     const RT x = (RT)rc.x(j), xr = x - ypr, p2 = psi[j].re * psi[j].re + psi[j].im * psi[j].im;
                     d2[0] += (double)(2 * x * xr * p2);
                     d2[1] += (double)(x * xr * xr * p2);
-                });
+                }
                 step_sum<2>(d2);
                 QC_STAMP(6);
                 const double kRed = -(c1 + c2) * g4, kDpd = (c3 + c4 - c5) * beta - kRed * yp, k5 = c5 * beta;

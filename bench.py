@@ -110,6 +110,36 @@ def latest_profile(workload: str, sha: str):
     return best
 
 
+def latest_sq(workload: str, sha: str):
+    """The newest committed SQ instruction-mix summary (profiles/*_sq.json, tools/sq_summary.py) of this
+    workload on this same library build, or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("lib_sha") == sha:
+            best = d
+    return best
+
+
+def executed_flops_per_elem(sq: dict, fp32: bool):
+    """Executed floating-point operations per state element and env-step, from the SQ counters of the same
+    library on the same workload: SQ_INSTS_VALU_FLOPS_FP64 / _FP32 count the flops of each wave instruction
+    per lane (an FMA 2, a packed v_pk_fma_f32 4; the fp64 counter equals 2 FMA + MUL + ADD of the instruction
+    counts exactly), x 64 lanes / N rows. Without those counters: fp64 from the FMA / MUL / ADD instruction
+    counts; fp32 None (a packed instruction counts once there)."""
+    d, N = sq.get("derived", {}), sq["N"]
+    f = d.get("fp32_flops_counter_per_wave_step" if fp32 else "fp64_flops_counter_per_wave_step")
+    if f:
+        return 64.0 * f / N
+    if not fp32 and d.get("f64_flops_per_wave_step_from_insts"):
+        return d["f64_flops_per_wave_step_from_insts"] / N
+    return None
+
+
 def dry_run(world: int, rank: int):
     import torch
     import torch.distributed as dist
@@ -241,6 +271,9 @@ def main():
         # separate "binding" object, in TFLOP/s against the FP64 (FP32 for C5) vector peak
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": None,
+                     # "bound" is the north-star yardstick's (algorithmic psi bytes vs HBM peak); the pipe that
+                     # actually limits k_step is "limiter" (= binding.bound)
+                     "limiter": "fp32_valu" if fp32 else "fp64_valu",
                      "yardstick": f"{int(bpe)}*N B/env-step (psi read+write) x env-steps per launch / k_step time "
                                   "(SURVEY §8d north-star yardstick; the kernel keeps psi on chip, measured_gbs is "
                                   "the real HBM traffic rate)",
@@ -259,6 +292,17 @@ def main():
         res["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC, profiles/%s_summary.json)" % prof["tag"]
         res["roofline"]["algorithmic_bytes_per_launch"] = bpe * N * per_launch_units
         res["roofline"]["measured_gbs"] = prof["hbm_bytes_per_launch"] / (kern_ms * 1e-3) / 1e9
+    # the executed-flop count of the same library on this workload (rocprofv3 SQ counters), beside the nominal
+    # per-element count of SURVEY §8d
+    b = res["roofline"]["binding"]
+    b["executed_flops_per_elem"] = b["executed_frac"] = b["executed_achieved"] = None
+    sq = latest_sq(res["config"]["workload"], sha)
+    if sq is not None:
+        fe = executed_flops_per_elem(sq, fp32)
+        if fe:
+            ex = fe * N * per_launch_units / (kern_ms * 1e-3)
+            b.update(executed_flops_per_elem=fe, executed_achieved=ex / 1e12, executed_frac=ex / peak_valu,
+                     executed_source="profiles/%s_sq.json" % sq["tag"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds, args.cpu_threads)

@@ -298,19 +298,10 @@ __global__ __launch_bounds__(1024) void k_actor_prep(const float* W, const float
 // cache line: 4.6 M partial-line writes per chunk). NT column tiles per wave: every weight fragment
 // feeds NT MFMAs, every input value MT. (A polyphase activation layout that turns the stride-S gathers into
 // contiguous runs was measured: conv2/conv3 unchanged, conv1's scattered stores +23 %; not kept.)
-#ifndef QCART_MCONV_NT
-#define QCART_MCONV_NT 2, 2, 1
-#endif
-constexpr int kNTs[3] = {QCART_MCONV_NT};
+constexpr int kNTs[3] = {QCART_MCONV_NT};   // (knob defaults: qcart_expt.hpp)
 constexpr int kNT1 = kNTs[0], kNT2 = kNTs[1], kNT3 = kNTs[2];
-#ifndef QCART_MCONV_NA
-#define QCART_MCONV_NA 2, 1, 2
-#endif
 constexpr int kNAs[3] = {QCART_MCONV_NA};
 constexpr int kNA1 = kNAs[0], kNA2 = kNAs[1], kNA3 = kNAs[2];
-#ifndef QCART_MCONV_Q
-#define QCART_MCONV_Q 4, 4, 4
-#endif
 constexpr int kQs[3] = {QCART_MCONV_Q};   // k-steps per load batch
 constexpr int kQ1 = kQs[0], kQ2 = kQs[1], kQ3 = kQs[2];
 template <int CI, int KS, int S, int MT, int NT, int NA, int kQ>
@@ -456,12 +447,6 @@ __global__ __launch_bounds__(256) void k_mtr(const float* __restrict__ in, float
 // traffic per env is 8 / (MT * NT) tile streams of K: (MT, NT) = (8, 1) streams the 4.6 MB weight
 // matrix once per 32 envs — more than one XCD's L2, so from MALL. Buffer loads with wave-uniform
 // k-step offsets, batches of kQF k-steps loaded one batch ahead of the MFMAs.
-#ifndef QCART_MFC_MT
-#define QCART_MFC_MT 2
-#endif
-#ifndef QCART_MFC_NT
-#define QCART_MFC_NT 2
-#endif
 constexpr int kMfcMT = QCART_MFC_MT, kMfcNT = QCART_MFC_NT, kQF = 4;
 template <int MT, int NT>
 __global__ __launch_bounds__(256) void k_mfc(const float* __restrict__ X, int64_t x_ld, int K,

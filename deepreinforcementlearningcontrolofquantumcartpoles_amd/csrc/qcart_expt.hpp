@@ -3,8 +3,37 @@
 // -DQCART_STAMPS (a diagnostic build only, tools/diag_stamps.py): per-phase cycle shares of the step loop
 // (s_memtime at each QC_STAMP(phase) site of qcart_kernels.hpp), summed over all waves into qc_stamps[] and
 // read back by qc_debug_stamps. Without it every hook below expands to nothing.
+//
+// Experiment knobs: compile-time defaults of the shipped build that an experiment build (make expt / expt_actor
+// EXPT=-D...) overrides for an A/B. Each default is the measured winner.
 #pragma once
 #include <hip/hip_runtime.h>
+
+// step kernel: the largest rows-per-lane R (fp64-equivalent) that runs 8-wave workgroups (two waves per SIMD),
+// Fock families / grid
+#ifndef QCART_W8_MAX_R
+#define QCART_W8_MAX_R 8
+#endif
+#ifndef QCART_W8_MAX_RG
+#define QCART_W8_MAX_RG 9
+#endif
+// measurement actor (qcart_actor.hip): conv1..3 column tiles per wave, accumulator sets, k-steps per load batch;
+// fc1 output tiles x env tiles per wave
+#ifndef QCART_MCONV_NT
+#define QCART_MCONV_NT 2, 2, 1
+#endif
+#ifndef QCART_MCONV_NA
+#define QCART_MCONV_NA 2, 1, 2
+#endif
+#ifndef QCART_MCONV_Q
+#define QCART_MCONV_Q 4, 4, 4
+#endif
+#ifndef QCART_MFC_MT
+#define QCART_MFC_MT 2
+#endif
+#ifndef QCART_MFC_NT
+#define QCART_MFC_NT 2
+#endif
 
 #ifdef QCART_STAMPS
 namespace qcart {

@@ -469,7 +469,7 @@ __device__ __forceinline__ void h_rows(const cx<RT> (&v)[R], const Coef<FAM, R, 
 // padding rows (>= N) of a grid stencil output: the high word cleared (one v_cndmask instead of two per
 // fp64 value) leaves at most |lo| 2^-1074 < 2^-1042: the padding rows stay below 1e-313 through every
 // application, so what they feed back into the real rows' stencils (x hoff ~ 1e4) is ~270 orders of magnitude
-// below a real row's rounding; their squares vanish from the norm and the moments. QCART_PAD_EXACT: exact zeros.
+// below a real row's rounding; their squares vanish from the norm and the moments (exact zeros: C3 +3 %, C4 +3 %).
 __device__ __forceinline__ double pad_flush(double v, bool in) {
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
     const unsigned hi = in ? (unsigned)(u >> 32) : 0u;
@@ -512,13 +512,8 @@ __device__ __forceinline__ void grid_hf_rows(const cx<RT> (&v)[R], const RC& rc,
             re += cf.hoff[d] * (e[4 + j + d].re + e[4 + j - d].re);
             im += cf.hoff[d] * (e[4 + j + d].im + e[4 + j - d].im);
         }
-#ifdef QCART_PAD_EXACT
-        const bool in = (cf.base + j) < cf.N;   // keep padding rows exactly zero
-        f(j, in ? re : RT(0), in ? im : RT(0));
-#else
         const bool in = (cf.base + j) < cf.N;
         f(j, pad_flush(re, in), pad_flush(im, in));
-#endif
     }
 }
 
@@ -1095,19 +1090,20 @@ __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>&
 // kernel (C4) runs two waves per SIMD although its loop then keeps ~16 scratch accesses per step: 10.8 -> 10.2 ms
 // at 8 192 envs, 82.1 -> 76.2 ms at 65 536 (same call; with two-slot workgroups no round is padded — in round 2,
 // with per-slot padding, it lost at 8 192)
-#ifndef QCART_W8_MAX_RG
-#define QCART_W8_MAX_RG 9
-#endif
-#ifndef QCART_W8_MAX_R
-#define QCART_W8_MAX_R 8
-#endif
-// (fp32 rows take half the registers: R_eff = R * sizeof(RT) / 8)
+// (fp32 rows take half the registers: R_eff = R * sizeof(RT) / 8; the R bounds are qcart_expt.hpp knobs)
 template <int FAM, int R, typename RT = double>
 constexpr int kStepWaves =
     ((FAM <= 1 && R * (int)sizeof(RT) / 8 <= QCART_W8_MAX_R) || (FAM == 2 && R <= QCART_W8_MAX_RG)) ? 8 : 4;
 
 
-// The step loop's view of the kernel arguments (KAR: the kernarg segment through a pointer made opaque
+// lazy normalisation's guard: the carried scale scl = 1/|psi| multiplies up over the steps of a call; a
+// diverging env (past its Fail, where the scheme amplifies the top Fock levels / the grid edges, up to ~1e10
+// per 120 steps) would overflow |psi|^2 within a long call. Outside [2^-100, 2^100] (or NaN) the step folds scl
+// into psi (and X psi) and restarts at 1. A physical trajectory's norm drifts by O(dt) per step and never
+// gets there, so its arithmetic is unchanged.
+__device__ __forceinline__ bool lazy_rescale(double scl) { return !(scl > 0x1p-100 && scl < 0x1p100); }
+
+// The step loop's view of the kernel arguments (KAR:the kernarg segment through a pointer made opaque
 // every step, so its loads are not hoisted out of the loop; otherwise the by-value parameter itself)
 template <bool KAR>
 __device__ __forceinline__ decltype(auto) step_kargs(const KArgs& a) {
@@ -1321,8 +1317,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // scale that normalises them, sq = scl^2 (1 before the first step: psi is loaded normalised). The scheme
     // is linear in psi given its scalar means, and psi' /= |psi'| cancels any factor, so only the quadratic
     // forms inside a step (the Y+- means, the Phi+- products) take sq; the 2 R (Fock: 4 R) scaling multiplies
-    // per step move to one pass after the loop. Not in the fp32 kernel (C5), where the loop-carried scale
-    // costs the R = 32 kernel spills
+    // per step move to one pass after the loop (lazy_rescale bounds scl for diverging envs). Not in the fp32
+    // kernel (C5), where the loop-carried scale costs the R = 32 kernel spills
     constexpr bool LAZY = sizeof(RT) == 8;
     double scl = 1.0, sq = 1.0;
     QC_STAMP_BEGIN();
@@ -1522,6 +1518,12 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 for (int j = 0; j < R; ++j) psi[j] = acc[j];   // unnormalised (scl; the grid is fp64 only)
                 scl = scale;
                 sq = scale * scale;
+                if (lazy_rescale(scl)) {   // (wave-uniform; never on a physical trajectory)
+#pragma unroll
+                    for (int j = 0; j < R; ++j) psi[j] = C(psi[j].re * (RT)scl, psi[j].im * (RT)scl);
+                    scl = 1.0;
+                    sq = 1.0;
+                }
                 xbar = (RT)(a.w * (s[1] * scale) * scale);
                 const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
                 const bool f = stop * sc2 > thr2 || sbot * sc2 > thr2;
@@ -1802,6 +1804,15 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             if constexpr (LAZY) {
                 scl = scale;
                 sq = scale * scale;
+                if (lazy_rescale(scl)) {   // (wave-uniform; never on a physical trajectory)
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        psi[j] = C(psi[j].re * (RT)scl, psi[j].im * (RT)scl);
+                        xp[j] = C(xp[j].re * (RT)scl, xp[j].im * (RT)scl);
+                    }
+                    scl = 1.0;
+                    sq = 1.0;
+                }
             }
             xbar = (RT)(a.w * (s[1] * scale) * scale);
             // check_boundary_error: sqrt(sum |psi|^2) > thr, compared squared (no square roots)

@@ -28,12 +28,15 @@ def shard(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
 
 def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
     """Initialise the default process group from torchrun's env (127.0.0.1 rendezvous) whenever a
-    launcher set WORLD_SIZE — world 1 included, so a one-GPU run under a launcher still goes through
-    RCCL (the fake-cluster case of SURVEY §4 item 4). Without WORLD_SIZE nothing is initialised."""
+    launcher started this process — world 1 included, so a one-GPU run under a launcher still goes through
+    RCCL (the fake-cluster case of SURVEY §4 item 4). A launcher sets WORLD_SIZE and the rendezvous address;
+    a bare WORLD_SIZE=1 without MASTER_ADDR (a user's shell export) is no launcher: nothing is initialised,
+    as without WORLD_SIZE."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if "WORLD_SIZE" in os.environ and not dist.is_initialized():
+    launched = "WORLD_SIZE" in os.environ and (world > 1 or "MASTER_ADDR" in os.environ)
+    if launched and not dist.is_initialized():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"

@@ -37,15 +37,36 @@ def _start_rccl_child(config):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: longer CPU test")
-    if _selects_gpu(config) and os.path.exists("/dev/kfd"):
+    # only the controlling process of a session (pytest-xdist workers carry `workerinput`: each would start a
+    # child of its own)
+    if _selects_gpu(config) and os.path.exists("/dev/kfd") and not hasattr(config, "workerinput"):
         _start_rccl_child(config)
 
 
-def pytest_unconfigure(config):
+def _stop_rccl_child(config):
     h = getattr(config, "_qcart_rccl", None)
     if h is not None and h[0].poll() is None:
         h[0].kill()
         h[0].wait()
+    config._qcart_rccl = None
+
+
+@pytest.hookimpl(trylast=True)   # after -k / -m deselection
+def pytest_collection_modifyitems(session, config, items):
+    """The RCCL child runs alone on the GPU: its test (which waits for it) goes first, so every other GPU test
+    starts after the child has finished; a session that did not collect the test (a -k subset, another
+    path) stops the child before any test runs."""
+    if getattr(config, "_qcart_rccl", None) is None:
+        return
+    first = [it for it in items if "test_gpu_rccl.py" in it.nodeid]
+    if not first:
+        _stop_rccl_child(config)
+        return
+    items[:] = first + [it for it in items if "test_gpu_rccl.py" not in it.nodeid]
+
+
+def pytest_unconfigure(config):
+    _stop_rccl_child(config)
 
 
 @pytest.fixture(scope="session")

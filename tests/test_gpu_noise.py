@@ -272,3 +272,173 @@ def test_mt19937_zero_word_matches_mkl(oracle_mod):
     o.run_batch(ref, acts, ph.f_max, n, ph.dt, ph.gamma, noise=normals.reshape(B, n, 2).transpose(1, 0, 2).copy(),
                 n_threads=1)
     assert np.abs(got - ref).max() < 1e-12
+
+
+FIX3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mkl_v3.npz")
+
+
+def _fix3(name):
+    import json
+    with np.load(FIX3) as z:
+        c = json.loads(bytes(z[f"traj/{name}/params"]).decode())
+        d = {k.split("/")[-1]: z[k] for k in z.files if k.startswith(f"traj/{name}/")}
+    return c, d
+
+
+def _v3_physics(c, **kw):
+    ts = int(round(1 / c["dt"]))
+    if c["kind"] == "iho":
+        return cfg.DEFAULTS[cfg.IHO].with_(n_max=c["n_max"], omega=c["omega"], gamma=c["gamma"], time_steps=ts,
+                                           f_max=c["f_max"], **kw)
+    return cfg.DEFAULTS[cfg.QO].with_(x_max=c["x_max"], grid_size=c["h"], lambda_=c["lam"], mass=c["mass"],
+                                      gamma=c["gamma"], time_steps=ts, f_max=c["f_max"], **kw)
+
+
+@pytest.mark.parametrize("name", ["qo1025", "iho1024"])
+def test_dropin_set_seed_reproduces_mkl_reference_trajectory_v3(name):
+    """The large configurations' sizes through the drop-in (load, set_seed, 1000 step calls, get_moments):
+    C3's QO x_n = 1025 grid at dt 1/11520 and IHO N = 1024, against the MKL-call-ordered steppers
+    (mkl_v3.npz, make_mkl_fixtures_v3.py): psi to 1e-9 (grid weighted by sqrt(h)) after 100 / 500 / 1000
+    steps, every step's q and x_mean to 1e-9, Fail never raised, the grid's 20 moments to 1e-9 relative."""
+    c, d = _fix3(name)
+    ph = _v3_physics(c)
+    kw = ph.asdict()
+    fam = kw.pop("family")
+    sim = S.load(fam, **kw)
+    w = 1.0 if c["kind"] == "iho" else np.sqrt(c["h"])
+    sim.set_seed(int(c["seed"]))
+    state = d["psi0"].copy()
+    qs, xs, errs, merrs = [], [], [], []
+    snap = 0
+    for k in range(len(d["q"])):
+        F = (int(d["actions"][k // c["ci"]]) - 10) * (c["f_max"] / 10.)
+        q, xm, fail = sim.step(state, c["dt"], F, c["gamma"])
+        assert fail == 0, k
+        qs.append(q)
+        xs.append(xm)
+        if k + 1 in (100, 500, 1000):
+            errs.append(np.linalg.norm(state - d["psi"][snap]) * w)
+            if c["kind"] == "grid":
+                data = np.zeros(20)
+                sim.get_moments(state, data)
+                ref = d["moments"][snap]
+                merrs.append(np.abs(data - ref).max() / max(1.0, np.abs(ref).max()))
+            snap += 1
+    assert np.abs(np.array(qs) - d["q"]).max() < 1e-9
+    assert np.abs(np.array(xs) - d["x_mean"]).max() < 1e-9
+    assert max(errs) < 1e-9, errs
+    if merrs:
+        assert max(merrs) < 1e-9, merrs
+    print(f"{name}: |psi - psi_mkl| = {errs[-1]:.2e} after 1000 steps" + (f", moments {max(merrs):.1e}" if merrs else ""))
+
+
+def _batched_on_fixture(c, d, ph, B):
+    """B copies of the fixture's env through the batched Stepper (fused control-interval launches of the
+    config's own step kernel, every copy on MKL's MT19937 stream of the case's seed)."""
+    st = Stepper(ph, B, 0)
+    st.set_seed_mt19937([int(c["seed"])] * B)
+    psi = torch.from_numpy(np.tile(d["psi0"], (B, 1))).to(st.state_dtype).cuda()
+    qs, xs = [], []
+    k0, steps = 0, len(d["q"])
+    for a in d["actions"]:
+        n = min(c["ci"], steps - k0)
+        out = st.step(psi, torch.full((B,), int(a), dtype=torch.int32, device="cuda"), n, want_q=True)
+        assert int(out["fail_step"].max()) == 0
+        qs.append(out["q"].cpu().numpy())
+        xs.append(out["x_mean"].cpu().numpy())
+        k0 += n
+    return psi.cpu().numpy().astype(np.complex128), np.concatenate(qs), np.concatenate(xs)
+
+
+@pytest.mark.parametrize("name", ["qo1025", "iho1024"])
+def test_stepper_tracks_mkl_reference_trajectory_v3(name):
+    """The batched path at the large sizes — k_step<…, R = 17> (C3) / R = 16, fused 160 / 80-step launches,
+    8 envs per workgroup on one force slot — on MKL's stream: every copy equals the MKL-call-ordered
+    trajectory to 1e-9 in psi after 1000 steps and in every step's q / x_mean."""
+    c, d = _fix3(name)
+    B = 8
+    psi, q, xm = _batched_on_fixture(c, d, _v3_physics(c), B)
+    w = 1.0 if c["kind"] == "iho" else np.sqrt(c["h"])
+    err = np.linalg.norm(psi - d["psi"][-1], axis=1).max() * w
+    assert np.abs(q - d["q"][:, None]).max() < 1e-9
+    assert np.abs(xm - d["x_mean"][:, None]).max() < 1e-9
+    assert err < 1e-9, err
+    print(f"{name}: batched |psi - psi_mkl| = {err:.2e} after 1000 steps")
+
+
+# fp32 working precision (C5) against the fp64 MKL reference, 1000 steps at N = 2048: a complex64 state
+# carries ~6e-8 relative rounding per step; the measured drift stays below 1e-5 in psi
+FP32_MKL_TOL_PSI = 2e-5
+FP32_MKL_TOL_X = 2e-5
+
+
+def test_fp32_tracks_mkl_reference_trajectory_iho2048():
+    """C5's kernel (k_step<1, 32, 1, float>: IHO N = 2048, fp32 state and tables, fp64 reductions) on MKL's
+    MT19937 stream against the fp64 MKL-call-ordered trajectory (mkl_v3.npz iho2048, gamma 2 pi,
+    dt 1/11520): ||psi - psi_mkl||_2 < 2e-5 after 1000 steps and |x_mean - x_mean_mkl| < 2e-5 at every
+    step (the fp32 bound stated above), 8 copies per launch."""
+    c, d = _fix3("iho2048")
+    psi, q, xm = _batched_on_fixture(c, d, _v3_physics(c, precision=1), 8)
+    err = np.linalg.norm(psi - d["psi"][-1], axis=1).max()
+    xerr = np.abs(xm - d["x_mean"][:, None]).max()
+    print(f"iho2048 fp32: |psi - psi_mkl| = {err:.2e}, max |x_mean - ref| = {xerr:.2e} after 1000 steps")
+    assert err < FP32_MKL_TOL_PSI, err
+    assert xerr < FP32_MKL_TOL_X, xerr
+
+
+# simulate_10_steps of the harmonic and grid modules (HO/simulation.cpp:372-402, QO/simulation_quart.cpp:526-558):
+# (family, load params, force of call c, expect a Fail). The quartic cooling well confines the packet (no Fail);
+# the inverted quartic's packet falls off the grid at the end the force pushes it to, so the grid's two-ended
+# boundary test (QO/simulation_quart.cpp:559-565) is exercised at each end
+S10_CASES = {
+    "ho31": (cfg.HO, dict(n_max=31), lambda c: 5.0 if c >= 3 else 0.5, True),
+    "qo171": (cfg.QO, dict(), lambda c: 5.0 if (c // 10) % 2 == 0 else -5.0, False),
+    "iqo301_right": (cfg.IQO, dict(x_max=7.5), lambda c: 5.0, True),
+    "iqo301_left": (cfg.IQO, dict(x_max=7.5), lambda c: -5.0, True),
+}
+
+
+@pytest.mark.parametrize("name", list(S10_CASES))
+def test_dropin_simulate_10_steps_matches_oracle_other_modules(oracle_mod, name):
+    """simulate_10_steps for HO and the grid modules: ten go_one_step calls, the last step's (q, x_mean) and
+    the Fail test of the FINAL state only (HO: top-5 Fock amplitudes > 1e-3; grid: either end's 6 points >
+    5e-3) — against the oracle on the same MT19937 stream, call by call, up to and including the call where the
+    state first reaches the boundary."""
+    fam, params, force_of, expect_fail = S10_CASES[name]
+    sim = S.load(fam, **params)
+    ph = sim._impl.physics
+    seed = 11
+    sim.set_seed(seed)
+    mt = oracle_mod.MT19937(seed)
+    if ph.fock:
+        o = oracle_mod.OracleSystem(fam, n_max=ph.n_max, omega=ph.omega)
+        state = np.zeros(o.N, np.complex128)
+        state[0] = 1.0
+    else:
+        o = oracle_mod.OracleSystem(fam, x_max=ph.x_max, grid_size=ph.grid_size, lambda_=ph.lambda_, mass=ph.mass)
+        x = ph.grid_size * (np.arange(o.N) - o.N // 2)
+        state = (np.exp(-x * x / 4.) / (2 * pi) ** 0.25).astype(np.complex128)
+    ref = state.copy()
+    w = 1.0 if ph.fock else np.sqrt(ph.grid_size)
+    first_fail = None
+    n_calls = 400 if expect_fail else 30
+    for call in range(n_calls):
+        force = force_of(call)
+        q, xm, fail = sim.simulate_10_steps(state, ph.dt, force, ph.gamma)
+        for k in range(10):
+            q2, xm2, f2 = o.step(ref, ph.dt, force, ph.gamma, mt.normals(2))
+        assert abs(q - q2) < 1e-9 and abs(xm - xm2) < 1e-9, call
+        assert fail == f2, call
+        assert np.linalg.norm(state - ref) * w < 1e-9, call
+        if fail:
+            first_fail = call
+            break
+    if expect_fail:
+        assert first_fail is not None, "never reached the boundary"
+        if name.startswith("iqo"):
+            # the end the packet fell off
+            side = np.sign(o.x_expectation(ref))
+            assert side == (1 if name.endswith("right") else -1)
+    else:
+        assert first_fail is None
+    print(f"{name}: first Fail at call {first_fail}")

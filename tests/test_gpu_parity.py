@@ -634,3 +634,31 @@ def test_env_steps_grouping_bitwise(case):
         want = {0: psi0, 40: part, 80: full}[int(bz[e])]
         assert torch.equal(a[e], want[e]), e
     assert int(out["fail_step"][budget == 0].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("case,steps", [("iho512", 4000), ("iqo513", 6000)])
+def test_diverging_envs_stay_finite_in_long_calls(case, steps):
+    """Lazy normalisation carries psi unnormalised through a call; an env past its Fail diverges (IHO N = 512
+    at gamma 2 pi, dt 1/1440 blows up after ~700 steps; the inverted quartic's packet falls off its grid under full pushes),
+    and its carried scale would overflow within a long call. The kernel folds the scale back into psi once it
+    leaves [2^-100, 2^100] (lazy_rescale): psi stays finite and normalised, and the observation finite."""
+    ph = CASES[case]
+    B = 4
+    st = Stepper(ph, B, 0, seed=5)
+    psi = st.new_state()
+    if ph.fock:
+        st.reset(psi, 1, arg0=16)
+        acts = torch.tensor([0, 20, 10, 3], dtype=torch.int32, device="cuda")
+    else:
+        st.reset(psi, 2, arg0=0.0, arg1=0.0, arg2=1.0)
+        acts = torch.tensor([0, 20, 0, 20], dtype=torch.int32, device="cuda")
+    out = st.step(psi, acts, steps, want_fail=True, want_obs=True)
+    torch.cuda.synchronize()
+    p = psi.cpu().numpy()
+    assert np.all(np.isfinite(p))
+    assert np.all(np.isfinite(out["obs"].cpu().numpy()))
+    norms = wnorm(ph, p)
+    np.testing.assert_allclose(norms, 1.0, atol=1e-9)
+    if ph.fock:
+        assert int((out["fail_step"] > 0).sum()) >= 1
+    print(f"{case}: fail steps {out['fail_step'].tolist()}, norms {norms}")

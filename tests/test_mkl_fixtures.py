@@ -241,3 +241,59 @@ def test_boxmuller_zero_word_equals_mkl(fx2):
         got = mt.normals(len(ref))
         assert np.all(np.isfinite(got))
         assert np.all(np.abs(got - ref) <= 2 * np.spacing(np.abs(ref))), (got, ref)
+
+
+# ---- mkl_v3.npz: the same MKL-call-ordered pin at the large configurations' sizes (C3's x_n = 1025 grid at
+# dt 1/11520, IHO N = 1024 and C5's N = 2048; make_mkl_fixtures_v3.py)
+FIX3 = os.path.join(HERE, "golden", "mkl_v3.npz")
+V3_CASES = ["qo1025", "iho1024", "iho2048"]
+
+
+@pytest.fixture(scope="module")
+def fx3():
+    with np.load(FIX3) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("name", V3_CASES)
+def test_oracle_tracks_mkl_ordered_stepper_v3(fx3, name):
+    """mklref.GridMkl at QO x_n = 1025 (QO/simulation_quart.cpp:394-432,569-644) and mklref.IhoMkl at
+    IHO N = 1024 / 2048 (IHO/simulation_i.cpp:227-277,432-489), fed MKL's CBWR=COMPATIBLE stream of the
+    case's seed: the oracle agrees to 1e-9 in psi (grid weighted by sqrt(h)) after 1000 steps and in every
+    step's q and x_mean, on the fixture's normals and on its own MT19937 stream; Fail is never raised; the
+    grid's 20 moments of each MKL snapshot equal compute_statistics' to 1e-9 relative."""
+    c = json.loads(bytes(fx3[f"traj/{name}/params"]).decode())
+    if c["kind"] == "iho":
+        s = O.OracleSystem(O.IHO, n_max=c["n_max"], omega=c["omega"])
+        w = 1.0
+    else:
+        s = O.OracleSystem(O.QO, x_max=c["x_max"], grid_size=c["h"], lambda_=c["lam"], mass=c["mass"])
+        w = np.sqrt(c["h"])
+    acts, ci = fx3[f"traj/{name}/actions"], c["ci"]
+    assert len(set(acts.tolist())) > 2          # the force changes: several reset_ab tables are exercised
+    for source in ("fixture", "oracle_mt"):
+        if source == "fixture":
+            r = fx3[f"traj/{name}/noise"]
+        else:
+            r = O.MT19937(int(c["seed"])).normals(2 * len(fx3[f"traj/{name}/q"])).reshape(-1, 2)
+        psi = fx3[f"traj/{name}/psi0"].copy().reshape(1, -1)
+        qs, xs = [], []
+        k0 = 0
+        for a in acts:
+            n = min(ci, len(r) - k0)
+            fail, q, xm = s.run_batch(psi, np.array([a], np.int32), c["f_max"], n, c["dt"], c["gamma"],
+                                      noise=r[k0:k0 + n].reshape(n, 1, 2), want_q=True, n_threads=1)
+            assert fail[0] == 0
+            qs.append(q[:, 0])
+            xs.append(xm[:, 0])
+            k0 += n
+        q, xm = np.concatenate(qs), np.concatenate(xs)
+        assert np.abs(q - fx3[f"traj/{name}/q"]).max() < 1e-9, source
+        assert np.abs(xm - fx3[f"traj/{name}/x_mean"]).max() < 1e-9, source
+        err = np.linalg.norm(psi[0] - fx3[f"traj/{name}/psi"][-1]) * w
+        assert err < 1e-9, (source, err)
+    assert not fx3[f"traj/{name}/fail"].any()
+    if c["kind"] == "grid":
+        for snap, ref in zip(fx3[f"traj/{name}/psi"], fx3[f"traj/{name}/moments"]):
+            got = s.moments(snap)
+            assert np.abs(got - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max())

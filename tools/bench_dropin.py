@@ -2,26 +2,33 @@
 copies per call): the reference drivers' own call pattern, IHO/main_parallel.py:264.
 
     python tools/bench_dropin.py [--n-max 180] [--calls 2000]
+    python tools/bench_dropin.py --procs 1,8,16 [--seconds 5] [--n-max 180] [--kinds gpu,cpu] [--out FILE]
+
+--procs: the reference's process model (IHO/main_parallel.py:345-359: 30-40 actor processes, each with its
+own `simulation` module stepping one env): P independent processes, each `install()`ing the drop-in and calling
+`step` on one env, all on the same GPU, started together behind a file barrier; the aggregate is the sum of
+the processes' step calls/s over the common timed window. --kinds gpu,cpu adds the same P processes running the oracle
+(the CPU restatement, one env and one host core each — what the reference's own processes do) for comparison.
+The parent never touches the GPU; each process is a fresh child.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 from math import pi
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
-from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S  # noqa: E402
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--n-max", type=int, default=180)
-    ap.add_argument("--calls", type=int, default=2000)
-    args = ap.parse_args()
+def single(args):
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
     sim = S.load(cfg.IHO, n_max=args.n_max)
     sim.set_seed(1)
     state = np.zeros(args.n_max + 1, np.complex128)
@@ -38,6 +45,112 @@ def main():
         dtm = time.perf_counter() - t0
         out[name] = {"calls_per_s": n / dtm, "env_steps_per_s": n * per / dtm, "us_per_call": dtm / n * 1e6}
     print(json.dumps({"n_max": args.n_max, **out}))
+
+
+def worker(args):
+    """One actor process: the drivers' call sequence (install, set_seed, step per dt; force redrawn every 80
+    steps) on one env, timed after the go file appears."""
+    dt, gamma = 1 / 1440, 2 * pi
+    state = np.zeros(args.n_max + 1, np.complex128)
+    state[0] = 1.0
+    if args.kind == "gpu":
+        from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
+        sim = S.install("inverted_harmonic", device=0, n_max=args.n_max)
+        sim.set_seed(1000 + args.rank)
+
+        def step(F):
+            return sim.step(state, dt, F, gamma)
+    else:
+        from oracle import oracle as O
+        o = O.OracleSystem(O.IHO, n_max=args.n_max, omega=pi)
+        mt = O.MT19937(1000 + args.rank)
+
+        def step(F):
+            return o.step(state, dt, F, gamma, mt.normals(2))
+    for k in range(200):                              # warm-up (tables of the forces used below)
+        step(0.8 * ((k // 80) % 3 - 1))
+        if k % 80 == 79:
+            state[:] = 0
+            state[0] = 1.0
+    print("ready", flush=True)
+    while not os.path.exists(args.go):
+        time.sleep(0.001)
+    n = 0
+    t0 = time.time()
+    t_end = t0 + args.seconds
+    while True:
+        for _ in range(80):                            # one control interval per force
+            step(0.8 * ((n // 80) % 3 - 1))
+            n += 1
+        state[:] = 0                                   # restart the episode (keeps the env physical)
+        state[0] = 1.0
+        t = time.time()
+        if t >= t_end:
+            break
+    print(json.dumps({"rank": args.rank, "calls": n, "t0": t0, "t1": t}), flush=True)
+
+
+def fan_out(args, kind, P):
+    go = os.path.join(tempfile.mkdtemp(prefix="qcart_dropin_"), "go")
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    errs = [open(go + f".err{r}", "w+") for r in range(P)]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker", "--kind", kind, "--rank", str(r),
+                               "--go", go, "--seconds", str(args.seconds), "--n-max", str(args.n_max)],
+                              cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=errs[r], text=True)
+             for r in range(P)]
+
+    def fail(r):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        errs[r].seek(0)
+        raise RuntimeError(errs[r].read()[-2000:])
+    for r, p in enumerate(procs):                      # every process ready (module loaded, warmed up)
+        if not p.stdout.readline().startswith("ready"):
+            p.wait()
+            fail(r)
+    open(go, "w").close()
+    res = []
+    for r, p in enumerate(procs):
+        out, _ = p.communicate(timeout=args.seconds * 4 + 120)
+        if p.returncode != 0:
+            fail(r)
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    # the common window: every process was stepping throughout [max t0, min t1]; rates over each process' own
+    # window are summed (each window covers the common one)
+    agg = sum(r["calls"] / (r["t1"] - r["t0"]) for r in res)
+    overlap = min(r["t1"] for r in res) - max(r["t0"] for r in res)
+    return {"kind": kind, "procs": P, "step_calls_per_s": agg, "per_proc_calls_per_s": agg / P,
+            "us_per_call": P / agg * 1e6, "seconds": args.seconds, "overlap_s": overlap}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-max", type=int, default=180)
+    ap.add_argument("--calls", type=int, default=2000)
+    ap.add_argument("--procs", default="")
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--kinds", default="gpu", help="gpu,cpu: the drop-in and/or the oracle processes")
+    ap.add_argument("--out", default="")
+    ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--kind", default="gpu")
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--go", default="")
+    args = ap.parse_args()
+    if args.worker:
+        return worker(args)
+    if not args.procs:
+        return single(args)
+    rows = []
+    for kind in args.kinds.split(","):
+        for P in [int(x) for x in args.procs.split(",")]:
+            r = fan_out(args, kind, P)
+            print(json.dumps(r), flush=True)
+            rows.append(r)
+    res = {"n_max": args.n_max, "call": "simulation.step(state, 1/1440, F, 2 pi), F redrawn every 80 steps",
+           "model": "P independent actor processes, one env each (IHO/main_parallel.py:345-359)", "rows": rows}
+    if args.out:
+        json.dump(res, open(args.out, "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -1494,22 +1494,44 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             band_solve<KL, R, MODE, false, true, 64, SPD>(acc, tb, kf, kb, lane QC_SOLVE_STAMP_PASS);   // QO:622
             QC_STAMP(8);
             {
-                // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window
-                double s[2] = {0.0, 0.0}, pwin = 0.0, stop = 0.0, sbot = 0.0, ptop = 0.0, pbot = 0.0;
+                // normalise (QO:259-263) + next <x> + Fail (QO:559-565) + IQO outside-probability window. The lane's
+                // rows are summed high -> low, so the running sum at row j is the lane's suffix sum from j: the
+                // boundary bands and the window edges are suffix sums captured at (wave-uniform) rows, by an FMA with
+                // a 0 / 1 weight (no per-row lane predicates), the lanes between them add whole. One reduction for
+                // the norm, <x> and the window (QO reduces a zero).
+                constexpr int BND = 6;                            // the grid's boundary band (a.bnd_len)
+                constexpr int LB = (BND - 1) / R, JB = BND - LB * R;   // bottom band: lanes < LB whole, lane LB rows < JB
+                const int r0 = N - BND, lt = r0 / R, jt = r0 - lt * R;
+                const int wl = a.win_lo < 0 ? 0 : a.win_lo, wh = a.win_hi > 64 * R ? 64 * R : a.win_hi;
+                const bool won = win_on && wh > wl;
+                const int llo = wl / R, jlo = wl - llo * R, lhi = wh / R, jhi = wh - lhi * R;
+                double s[3] = {0.0, 0.0, 0.0}, ct = 0.0, cl = 0.0, ch = 0.0, cb = 0.0;
                 const auto rc = rowc();
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
+                for (int j = R - 1; j >= 0; --j) {
                     const double p2 = (double)(acc[j].re * acc[j].re + acc[j].im * acc[j].im);
-                    s[0] += p2;
+                    s[0] = j == R - 1 ? p2 : s[0] + p2;
                     s[1] += rc.x(j) * p2;
-                    const int r = base + j;
-                    if (r >= N - a.bnd_len && r < N) ptop += p2;
-                    if (r < a.bnd_len) pbot += p2;
-                    if (r >= a.win_lo && r < a.win_hi) pwin += p2;
+                    ct = fma(j == jt ? 1.0 : 0.0, s[0], ct);
+                    cl = fma(j == jlo ? 1.0 : 0.0, s[0], cl);
+                    ch = fma(j == jhi ? 1.0 : 0.0, s[0], ch);   // (jhi = R never matches: ch = 0)
+                    if (j == JB) cb = s[0];                      // compile-time row
                 }
-                for (int l = (N - a.bnd_len) / R; l <= (N - 1) / R; ++l) stop += readlane_d(ptop, l);
-                for (int l = 0; l <= (a.bnd_len - 1) / R; ++l) sbot += readlane_d(pbot, l);
-                step_sum<2>(s);
+                const double tot = s[0];
+                if (won) {
+                    const int l = lane;
+                    double pw = (l > llo && l < lhi) ? tot : 0.0;
+                    pw = l == llo ? (llo == lhi ? cl - ch : cl) : pw;
+                    pw = (l == lhi && llo != lhi) ? tot - ch : pw;
+                    s[2] = pw;
+                }
+                double stop = readlane_d(ct, lt), sbot = 0.0;
+                for (int l = lt + 1; l <= (N - 1) / R; ++l) stop += readlane_d(tot, l);
+#pragma unroll
+                for (int l = 0; l < LB; ++l) sbot += readlane_d(tot, l);
+                sbot += readlane_d(JB < R ? tot - cb : tot, LB);
+                step_sum<3>(s);
+                const double pwin = s[2];
                 double scale = __builtin_amdgcn_rsq(s[0]);
                 scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
                 scale = scale * (1.5 - 0.5 * s[0] * scale * scale);
@@ -1528,11 +1550,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 const double sc2 = scale * scale, thr2 = a.fail_thr * a.fail_thr;
                 const bool f = stop * sc2 > thr2 || sbot * sc2 > thr2;
                 if (f && fail == 0) fail = k + 1;
-                if (win_on && term < 0) {
-                    double sw[1] = {pwin};
-                    step_sum<1>(sw);
-                    if (1.0 - a.h * (sw[0] * scale) * scale > 0.5) term = k + 1;
-                }
+                if (won && term < 0 && 1.0 - a.h * (pwin * scale) * scale > 0.5) term = k + 1;
             }
         } else {
         // Live vectors are kept to at most five R-row complex vectors (plus one halo) at any point so
@@ -1769,7 +1787,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 for (int j = R - 1; j >= 0; --j) {
                     s[0] = dot_acc(s[0], j == R - 1, acc[j], acc[j]);
                     qx.add(j == R - 1, acc[j], xn[j]);
-                    if (j == jt) suf = s[0];
+                    suf = fma(j == jt ? 1.0 : 0.0, s[0], suf);   // (0 / 1 weight: an FMA, not a lane select)
                 }
                 s[1] = qx.sum();
                 const int l1 = (N - 1) / R;

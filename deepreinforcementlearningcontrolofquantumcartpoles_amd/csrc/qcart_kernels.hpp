@@ -729,6 +729,36 @@ template <int KL, bool FWD, int MODE, int LE, typename RT>
 __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& tb, uint32_t lv0, uint32_t lvp,
                                           int nlev) {
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
+    if constexpr (KL >= 4) {
+        // grid (kl = 4), at most 2 kept levels: the composites are whole-wave transfers (T_{k+1}(l) =
+        // T_k(l) T_k(l - 2^k), qcart_tables.cpp) and any transfer over >= 4 lanes is below kScanTol, so a
+        // Kogge-Stone over the whole wave with distances 1 and 2 (wave_shr / wave_shl by 1, twice for 2)
+        // reaches every lane that matters and needs no row carry: the carry's 16 composite reads and 16
+        // complex multiply-adds per scan drop out
+        if (nlev <= 2) {
+#pragma unroll
+            for (int lvl = 0; lvl < 2; ++lvl) {
+                if (lvl < nlev) {
+                    cx<RT> T[KL * KL];
+#pragma unroll
+                    for (int e = 0; e < KL * KL; ++e)
+                        T[e] = FWD ? tb.compf(lv0 + (uint32_t)(lvl * KL * KL + e) * CE) : tb.comp(lv0 + (uint32_t)(lvl * KL * KL + e) * CE);
+                    cx<RT> p[KL];
+#pragma unroll
+                    for (int k = 0; k < KL; ++k) {
+                        if (FWD) p[k] = lvl == 0 ? C(shr1(s[k].re), shr1(s[k].im)) : C(shr<2>(s[k].re), shr<2>(s[k].im));
+                        else p[k] = lvl == 0 ? C(shl1(s[k].re), shl1(s[k].im)) : C(shl<2>(s[k].re), shl<2>(s[k].im));
+                    }
+#pragma unroll
+                    for (int i = 0; i < KL; ++i)
+#pragma unroll
+                        for (int k = 0; k < KL; ++k) s[i] = cmac(s[i], T[i * KL + k], p[k]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            return;
+        }
+    }
     // composites are read level by level (KL = 4: 16 complex per level; all levels at once would
     // not fit the register file), fenced for KL = 4 so the next level's reads are not hoisted
 #pragma unroll
@@ -1194,11 +1224,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         }
         if constexpr (MODE == 2 || MODE == 4) {   // the kept composite levels at their fixed places (band_solve)
             constexpr uint32_t CB = KL * KL * CE, NL = (uint32_t)mode2_levels(KL);
+            // (the grid's <= 2-level scans run over the whole wave without the row prefix: scan_rows)
+            constexpr bool PFX = KL < 4;
             copy(SL.tf, SL.tf, (uint32_t)kf * CB);
-            copy(SL.tf + 6u * CB, SL.tf + NL * CB, CB);
+            if (PFX) copy(SL.tf + 6u * CB, SL.tf + NL * CB, CB);
             if constexpr (MODE == 2) {
                 copy(SL.tb, SL.tf + (NL + 1u) * CB, (uint32_t)kb * CB);
-                copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
+                if (PFX) copy(SL.tb + 6u * CB, SL.tf + (2u * NL + 1u) * CB, CB);
             }
         }
         static_assert(!(FAM == 2 && MODE == 3 && grid_rows_in_lds(R)), "two-slot blocks carry no row constants");

@@ -17,6 +17,27 @@
 #ifndef QCART_W8_MAX_RG
 #define QCART_W8_MAX_RG 9
 #endif
+// band solve: the fp32 Fock kernels' whole-wave Kogge-Stone (no row carry) for up to this many kept levels (0: off;
+// 3: C5 -1.6 %)
+#ifndef QCART_WKS_F32
+#define QCART_WKS_F32 3
+#endif
+// step kernel: the fp32 R = 32 kernel's Y+- means in two reductions (1; C5 46.7 -> 43.2 ms) or one (0)
+#ifndef QCART_SPLITM
+#define QCART_SPLITM 1
+#endif
+// step kernel: the fp32 R = 32 kernel recomputes rel after the Horner (1) or holds it through (0)
+#ifndef QCART_RECREL
+#define QCART_RECREL 0
+#endif
+// step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
+// R = 17 (C3) / fp32 R = 32 (C5) kernels
+#ifndef QCART_KAR_G17
+#define QCART_KAR_G17 0
+#endif
+#ifndef QCART_KAR_F32
+#define QCART_KAR_F32 0
+#endif
 // measurement actor (qcart_actor.hip): conv1..3 column tiles per wave, accumulator sets, k-steps per load batch;
 // fc1 output tiles x env tiles per wave
 #ifndef QCART_MCONV_NT

@@ -729,15 +729,16 @@ template <int KL, bool FWD, int MODE, int LE, typename RT>
 __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& tb, uint32_t lv0, uint32_t lvp,
                                           int nlev) {
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>);   // bytes of one lane-interleaved complex run
-    if constexpr (KL >= 4) {
-        // grid (kl = 4), at most 2 kept levels: the composites are whole-wave transfers (T_{k+1}(l) =
-        // T_k(l) T_k(l - 2^k), qcart_tables.cpp) and any transfer over >= 4 lanes is below kScanTol, so a
-        // Kogge-Stone over the whole wave with distances 1 and 2 (wave_shr / wave_shl by 1, twice for 2)
-        // reaches every lane that matters and needs no row carry: the carry's 16 composite reads and 16
-        // complex multiply-adds per scan drop out
-        if (nlev <= 2) {
+    // whole-wave Kogge-Stone without the row carry, for few kept levels: the composites are whole-wave transfers
+    // (T_{k+1}(l) = T_k(l) T_k(l - 2^k), qcart_tables.cpp) and any transfer over >= 2^nlev lanes is below
+    // kScanTol, so distances 1, 2 (, 4) across the whole wave (wave_shr / wave_shl by 1, chained) reach every lane
+    // that matters: the carry's composite reads and multiply-adds drop out. The grid (kl = 4, <= 2 levels: the
+    // carry is 16 composite reads and 16 complex multiply-adds); the fp32 Fock kernel with <= QCART_WKS_F32 levels
+    constexpr int NLW = KL >= 4 ? 2 : (sizeof(RT) == 4 ? QCART_WKS_F32 : 0);
+    if constexpr (NLW > 0) {
+        if (nlev <= NLW) {
 #pragma unroll
-            for (int lvl = 0; lvl < 2; ++lvl) {
+            for (int lvl = 0; lvl < NLW; ++lvl) {
                 if (lvl < nlev) {
                     cx<RT> T[KL * KL];
 #pragma unroll
@@ -746,8 +747,10 @@ __device__ __forceinline__ void scan_rows(cx<RT> (&s)[KL], const Tab<MODE, RT>& 
                     cx<RT> p[KL];
 #pragma unroll
                     for (int k = 0; k < KL; ++k) {
-                        if (FWD) p[k] = lvl == 0 ? C(shr1(s[k].re), shr1(s[k].im)) : C(shr<2>(s[k].re), shr<2>(s[k].im));
-                        else p[k] = lvl == 0 ? C(shl1(s[k].re), shl1(s[k].im)) : C(shl<2>(s[k].re), shl<2>(s[k].im));
+                        if (FWD) p[k] = lvl == 0 ? C(shr1(s[k].re), shr1(s[k].im))
+                                      : lvl == 1 ? C(shr<2>(s[k].re), shr<2>(s[k].im)) : C(shr<4>(s[k].re), shr<4>(s[k].im));
+                        else p[k] = lvl == 0 ? C(shl1(s[k].re), shl1(s[k].im))
+                                  : lvl == 1 ? C(shl<2>(s[k].re), shl<2>(s[k].im)) : C(shl<4>(s[k].re), shl<4>(s[k].im));
                     }
 #pragma unroll
                     for (int i = 0; i < KL; ++i)
@@ -1339,7 +1342,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
-    constexpr bool KAR = !(FAM == 2 && R >= 17) && !(sizeof(RT) == 4 && R >= 32);
+    constexpr bool KAR = (!(FAM == 2 && R >= 17) || QCART_KAR_G17) && (!(sizeof(RT) == 4 && R >= 32) || QCART_KAR_F32);
     // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
     // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
@@ -1592,6 +1595,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         //   C  acc = psi + kA rel + k2 D1 + u + mirror(D1);  psi <- Y0 = psi + dt D1
         //   D  Y- branch, then Y+ branch (D1ImRe IHO:301-318, D2 IHO:320-333)
         //   E  Phi+- means from <Y+, X rel+> products (no X Phi+- applications)
+        // RECREL (the fp32 R = 32 kernel): rel is recomputed after the Horner instead of held through it (one
+        // more X application, 64 VGPRs fewer live in the term7 phase; QCART_RECREL)
+        constexpr bool RECREL = sizeof(RT) == 4 && R >= 32 && QCART_RECREL;
         cx<RT> acc[R], rel[R], D1[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
@@ -1627,6 +1633,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b2r * D1[j].re, acc[j].im + b2r * D1[j].im);
             hf(t, acc);
             hf(acc, t);
+            if constexpr (RECREL) {   // rel = (X - xbar) psi again (psi not yet updated): not held through the Horner
+                apply_x<FAM, R>(psi, rel, cf, lnv);
+#pragma unroll
+                for (int j = 0; j < R; ++j) rel[j] = C(rel[j].re - xbar * psi[j].re, rel[j].im - xbar * psi[j].im);
+            }
             const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2);
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -1680,8 +1691,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             if constexpr (FXL) return *(const RT*)(tb.lds + tb.vr + lds_fx + (R + 1 + j) * 64 * (int)sizeof(RT));
             else return cf.xu[j] * cf.xu[j] + cf.xu[j + 1] * cf.xu[j + 1];
         };
+        // SPLITM (the fp32 R = 32 kernel, one wave per SIMD): the Y- and Y+ means in two reductions, so that Y-,
+        // X Y- and X Y+ (64 VGPRs each) are never live together (QCART_SPLITM)
+        constexpr bool SPLITM = sizeof(RT) == 4 && R >= 32 && QCART_SPLITM;
         cx<RT> xYp[R];
-        double yp, ym, s1p;
+        double yp = 0.0, ym, s1p = 0.0;
         {
             cx<RT> Ym[R], xYm[R];
 #pragma unroll
@@ -1690,18 +1704,28 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 psi[j] = C(psi[j].re + kY * rel[j].re, psi[j].im + kY * rel[j].im);   // Y+
             }
             apply_x<FAM, R>(Ym, xYm, cf, lnv);
-            apply_x<FAM, R>(psi, xYp, cf, lnv);
-            RowDot<RT> q0, q1;
+            if constexpr (SPLITM) {
+                // the Y- mean alone: X Y+ is formed after the Y- branch, when Y- and X Y- are dead
+                RowDot<RT> q1;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-                q0.add(j == 0, psi[j], xYp[j]);
-                q1.add(j == 0, Ym[j], xYm[j]);
+                for (int j = 0; j < R; ++j) q1.add(j == 0, Ym[j], xYm[j]);
+                double sm[1] = {q1.sum()};
+                step_sum<1>(sm, lnv);
+                ym = (a.w * sq) * sm[0];
+            } else {
+                apply_x<FAM, R>(psi, xYp, cf, lnv);
+                RowDot<RT> q0, q1;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    q0.add(j == 0, psi[j], xYp[j]);
+                    q1.add(j == 0, Ym[j], xYm[j]);
+                }
+                double sm[2] = {q0.sum(), q1.sum()};
+                step_sum<2>(sm, lnv);
+                yp = (a.w * sq) * sm[0];
+                ym = (a.w * sq) * sm[1];
+                s1p = sm[0];
             }
-            double sm[2] = {q0.sum(), q1.sum()};
-            step_sum<2>(sm, lnv);
-            yp = (a.w * sq) * sm[0];
-            ym = (a.w * sq) * sm[1];
-            s1p = sm[0];
             const RT ymr = (RT)ym;
             if constexpr (X2H) {
                 // acc -= (c1-c6) (-i H_F Y-) + kRe X rel- + kDm rel-, X rel- = al H Y- + d Y- - ym X Y-, rel- = X Y- - ym Y-:
@@ -1732,6 +1756,16 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             for (int j = 0; j < R; ++j)
                 acc[j] = C(acc[j].re + kRe * Ym[j].re + kDm * xYm[j].re, acc[j].im + kRe * Ym[j].im + kDm * xYm[j].im);
             }
+        }
+        if constexpr (SPLITM) {
+            apply_x<FAM, R>(psi, xYp, cf, lnv);
+            RowDot<RT> q0;
+#pragma unroll
+            for (int j = 0; j < R; ++j) q0.add(j == 0, psi[j], xYp[j]);
+            double sm[1] = {q0.sum()};
+            step_sum<1>(sm, lnv);
+            yp = (a.w * sq) * sm[0];
+            s1p = sm[0];
         }
         QC_STAMP(4);
         if constexpr (X2H) {

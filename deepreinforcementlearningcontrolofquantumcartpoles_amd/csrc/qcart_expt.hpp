@@ -30,6 +30,10 @@
 #ifndef QCART_RECREL
 #define QCART_RECREL 0
 #endif
+// step kernel: the fp32 mirror update as packed v_pk_fma (1; C5 -0.6 %) or scalar FMAs (0)
+#ifndef QCART_PKMIR
+#define QCART_PKMIR 1
+#endif
 // step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
 // R = 17 (C3) / fp32 R = 32 (C5) kernels
 #ifndef QCART_KAR_G17

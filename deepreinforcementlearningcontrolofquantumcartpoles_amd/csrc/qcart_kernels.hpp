@@ -1651,7 +1651,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  (SURVEY App. C H1); the band
             // reads go in batches of MB bands fenced from the arithmetic so each batch is in flight at once
             if (a.mirror) {
-                constexpr int MB = 1;
+                constexpr int MB = 1;   // bands per batch of reads (fp32 R = 32 with 2: 42.4 -> 50.7 ms, spills)
                 cx<RT> lo[10];
                 make_lo<R, 10>(D1, lo, lnv);
 #pragma unroll
@@ -1669,7 +1669,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                             const int d = MB * h + dd + 1;
                             const cx<RT> dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
                                                        : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
-                            acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
+                            if constexpr (kPk<RT> && QCART_PKMIR) {   // acc + m (-i dv): one v_pk_fma (op_sel swap, neg_hi)
+                                acc[j] = CV(__builtin_elementwise_fma((v2f){mv[dd][j], -mv[dd][j]}, dv.v.yx, acc[j].v));
+                            } else {
+                                acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
+                            }
                         }
                 }
             }

@@ -1026,17 +1026,36 @@ __device__ __forceinline__ void grid_p(const cd (&v)[R], cd (&o)[R], double pbar
     cd e[R + 8];
     make_ext<R, 4>(v, e, lane);
     const double sd[5] = {0.0, 672.0 / 840.0, -168.0 / 840.0, 32.0 / 840.0, -3.0 / 840.0};
+    // the full antisymmetric band for every row, then (rows within 8 of the top only, a lane-divergent branch the
+    // wave skips when no lane takes it) the couplings the reference's truncated loops leave out: upper (r, r+d)
+    // for r > N-1-2d, mirrored lower (r, r-d) for r > N-1-d. (Selecting a zero coefficient per row and distance
+    // instead held 2 x 4 x R selected doubles in registers across the moments' p-power passes and spilled the
+    // R = 9 kernel's epilogue: ~60 scratch stores per lane.)
+    double dl[5];
+#pragma unroll
+    for (int d = 1; d <= 4; ++d) dl[d] = sd[d] * inv_h;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const int r = base + j;
         double re = 0.0, im = 0.0;
 #pragma unroll
         for (int d = 1; d <= 4; ++d) {
-            const double dl = sd[d] * inv_h;
-            const double up = (r <= N - 1 - 2 * d) ? dl : 0.0;
-            const double dn = (r <= N - 1 - d) ? dl : 0.0;
-            re += up * e[4 + j + d].re - dn * e[4 + j - d].re;
-            im += up * e[4 + j + d].im - dn * e[4 + j - d].im;
+            re += dl[d] * (e[4 + j + d].re - e[4 + j - d].re);
+            im += dl[d] * (e[4 + j + d].im - e[4 + j - d].im);
+        }
+        const int k = N - 1 - r;
+        if (k < 8) {
+#pragma unroll
+            for (int d = 1; d <= 4; ++d) {
+                if (k < 2 * d) {
+                    re -= dl[d] * e[4 + j + d].re;
+                    im -= dl[d] * e[4 + j + d].im;
+                }
+                if (k < d) {
+                    re += dl[d] * e[4 + j - d].re;
+                    im += dl[d] * e[4 + j - d].im;
+                }
+            }
         }
         // (-i) * (re + i im) - pbar v
         const bool in = r < N;

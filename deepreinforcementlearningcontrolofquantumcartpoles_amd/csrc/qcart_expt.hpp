@@ -30,9 +30,10 @@
 #ifndef QCART_RECREL
 #define QCART_RECREL 0
 #endif
-// step kernel: the fp32 mirror update as packed v_pk_fma (1; C5 -0.6 %) or scalar FMAs (0)
+// step kernel: the fp32 mirror update as packed v_pk_fma (1: C5 -0.6 %, but 17 spilled registers whose scratch
+// footprint adds 0.11 GB of HBM writes per launch) or scalar FMAs (0: no spills, psi once out)
 #ifndef QCART_PKMIR
-#define QCART_PKMIR 1
+#define QCART_PKMIR 0
 #endif
 // step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
 // R = 17 (C3) / fp32 R = 32 (C5) kernels

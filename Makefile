@@ -48,7 +48,7 @@ NAME ?= expt
 TU ?= qcart_k_iho
 expt: $(OBJS)
 	@mkdir -p $(CSRC)/build_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(if $(filter qcart_k_grid,$(TU)),,$(KFLAGS)) $(if $(filter qcart_k_f32,$(TU)),-fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED,) $(EXPT) -c $(CSRC)/$(TU).hip -o $(CSRC)/build_$(NAME)/$(TU).o
+	$(HIPCC) $(HIPFLAGS) $(if $(filter qcart_k_grid,$(TU)),-ffp-contract=fast,$(KFLAGS)) $(if $(filter qcart_k_f32,$(TU)),-fno-slp-vectorize -fms-extensions -DQCART_F32_PACKED,) $(EXPT) -c $(CSRC)/$(TU).hip -o $(CSRC)/build_$(NAME)/$(TU).o
 	$(HIPCC) $(HIPFLAGS) -shared -o $(PKG)/libqcart_$(NAME).so $(CSRC)/build_$(NAME)/$(TU).o $(filter-out $(CSRC)/build/$(TU).o,$(OBJS))
 # actor experiment builds: make expt_actor EXPT='-DQCART_MCONV_Q=4' NAME=q4
 expt_actor:

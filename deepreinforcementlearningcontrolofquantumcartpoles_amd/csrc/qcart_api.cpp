@@ -242,8 +242,10 @@ KArgs base_args(const qc_handle* h) {
                                   : (grid_rows_in_lds(op.R) ? (size_t)2 * op.R * kWave * 8 : 0);
         // MODE 4 (grid R >= 17): the forward levels + prefix only, beside the row constants
         const size_t t4 = L.tf + (size_t)(NL + 1) * op.kl * op.kl * op.lanes * es;
-        const bool m4 = !op.fock && !f32 && grid_rows_in_lds(op.R) && lf <= NL && t4 + fx <= 160 * 1024;
-        int mode = (t2 + fx <= 160 * 1024 && lf <= NL && lb <= NL) ? 2 : m4 ? 4 : (t1 + fx <= 160 * 1024 ? 1 : 0);
+        // fp64: each wave's noise buffer (kNzLds) after the image(s)
+        const size_t nzb = f32 ? 0 : (size_t)h->wpb * kNzLds, cap = 160 * 1024 - nzb;
+        const bool m4 = !op.fock && !f32 && grid_rows_in_lds(op.R) && lf <= NL && t4 + fx <= cap;
+        int mode = (t2 + fx <= cap && lf <= NL && lb <= NL) ? 2 : m4 ? 4 : (t1 + fx <= cap ? 1 : 0);
         if (const char* e = std::getenv("QCART_TAB_MODE")) {   // a cap: 0 < 1 < 4 < 2 in LDS use
             const int c = std::atoi(e);
             if (mode != 4 || c < 2) mode = std::min(mode, c);
@@ -255,6 +257,11 @@ KArgs base_args(const qc_handle* h) {
         if (h->dual_img && mode >= 1) {
             a.lds_img = h->dual_img;
             a.lds_bytes = std::max(a.lds_bytes, 2u * h->dual_img);
+        }
+        a.lds_nz = 0;
+        if (mode >= 1 && nzb) {
+            a.lds_nz = (a.lds_bytes + 15u) & ~15u;
+            a.lds_bytes = a.lds_nz + (uint32_t)nzb;
         }
     }
     a.precision = p.precision;

@@ -35,6 +35,20 @@
 #ifndef QCART_PKMIR
 #define QCART_PKMIR 0
 #endif
+// step kernel: the 64-step noise refill parked in a 1 KiB per-wave LDS buffer, read back one step at a time (1), or
+// held in 4 VGPRs across the step loop (0) — fp64 kernels with LDS tables (MODE >= 1)
+#ifndef QCART_NZ_LDS
+#define QCART_NZ_LDS 1
+#endif
+// noise refill: its polynomial constants defined in place by VGPR (2) or SGPR (1; miscompiles the grid R = 17
+// MODE 0 kernel) asm, or plain literals (0: hoisted and spilled); the own sin/cos(pi t) (1) or the library
+// sincospi (0)
+#ifndef QCART_KC
+#define QCART_KC 2
+#endif
+#ifndef QCART_SINCOS_OWN
+#define QCART_SINCOS_OWN 1
+#endif
 // step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
 // R = 17 (C3) / fp32 R = 32 (C5) kernels
 #ifndef QCART_KAR_G17

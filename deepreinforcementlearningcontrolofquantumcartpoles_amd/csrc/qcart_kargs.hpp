@@ -47,6 +47,8 @@ constexpr int mode2_levels(int kl) { return kl >= 4 ? 2 : 4; }
 // instead of holding them in registers: the R = 17 kernel, whose step spills (for R <= 9 the registers
 // are there and the LDS reads cost more than they save: C4 12.6 -> 14.9 ms, C3 29.4 -> 27.9 ms)
 constexpr bool grid_rows_in_lds(int R) { return R >= 17; }
+// bytes of LDS per wave for the step loop's noise refill (64 steps x 2 normals): fp64 kernels with LDS tables
+constexpr uint32_t kNzLds = 1024;
 
 struct KArgs {
     // state and I/O (device pointers)
@@ -83,6 +85,7 @@ struct KArgs {
     uint32_t n_mixed;          // capacity of two-slot blocks (0: none; launch_step DUAL); grid n_mixed + n_blocks
     const int32_t* n_mixed_used;   // device: k_group's two-slot workgroup count (blocks [0, it) run them)
     uint32_t lds_img;          // bytes of one slot's MODE 3 image (tables + H_F force coefficients)
+    uint32_t lds_nz;           // LDS offset of the per-wave noise buffers (fp64, tab_mode >= 1: kNzLds bytes per wave)
     // physics scalars
     double dt, sqrt_dt, gamma, g4, beta, inv_sqrt2g, w, inv_sqrt_w, c, h;
     double a2, a3, a4, a5;     // Horner coefficients dt^3/12, dt^4/24, dt^5/80, dt^6/360

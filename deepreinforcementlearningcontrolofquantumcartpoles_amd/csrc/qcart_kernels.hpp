@@ -631,6 +631,31 @@ __device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1
 // natural log on (0, 1] by the classic argument-reduction + Lg1..Lg7 minimax scheme (fdlibm
 // e_log.c, < 1 ulp): small and table-free, so the noise refill does not drag a constant table into
 // private memory (the library log did: ~1 GB of scratch traffic per metric launch)
+// KC(x): the fp64 constant x defined where it is used, by an asm statement with no inputs that writes its two
+// halves (v_mov_b32 x 2), so nothing of it is loop-invariant to the optimiser. Written as plain literals, the
+// noise refill's polynomial constants were hoisted to the kernel entry, and the kernels at their register limit
+// spilled them (C4: 108 B of scratch per lane, ~0.1 GB of HBM traffic per launch). The SGPR form (QCART_KC = 1:
+// s_mov_b32 pairs, or a tied "+s" operand on the literal) miscompiles the R = 17 grid kernel's MODE 0
+// instantiation at its 106-SGPR limit — halves of the constants reloaded from the wrong SGPR-spill lanes, NaN in
+// test_table_placements_bitwise_equal[qo1025] — so the halves go through VGPRs (a few VALU moves per 64 steps).
+constexpr uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+template <uint64_t B>
+__device__ __forceinline__ double kc_bits() {
+#if QCART_KC == 0
+    return __builtin_bit_cast(double, B);
+#else
+    uint32_t lo, hi;
+#if QCART_KC == 2
+    asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((int32_t)(uint32_t)B),
+                 "i"((int32_t)(uint32_t)(B >> 32)));
+#else
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi) : "i"((int32_t)(uint32_t)B),
+                 "i"((int32_t)(uint32_t)(B >> 32)));
+#endif
+    return __hiloint2double((int)hi, (int)lo);
+#endif
+}
+#define KC(x) kc_bits<dbits(x)>()
 __device__ __forceinline__ double log_unit(double x) {
     int k;
     double m = frexp(x, &k);                       // x = m 2^k, m in [0.5, 1)
@@ -640,11 +665,44 @@ __device__ __forceinline__ double log_unit(double x) {
     }
     const double f = m - 1.0;
     const double s = f / (2.0 + f), z = s * s, w = z * z;
-    const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-    const double t2 = z * (6.666666666666735130e-01 +
-                           w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+    const double t1 = w * (KC(3.999999999940941908e-01) + w * (KC(2.222219843214978396e-01) + w * KC(1.531383769920937332e-01)));
+    const double t2 = z * (KC(6.666666666666735130e-01) +
+                           w * (KC(2.857142874366239149e-01) + w * (KC(1.818357216161805012e-01) + w * KC(1.479819860511658591e-01))));
     const double Rr = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
-    return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + Rr) + dk * 1.90821492927058770002e-10)) - f);
+    return dk * KC(6.93147180369123816490e-01) - ((hfsq - (s * (hfsq + Rr) + dk * KC(1.90821492927058770002e-10))) - f);
+}
+
+// sin(pi t), cos(pi t) for t in [0, 2] (the Box-Muller angle 2 pi u2 as pi (2 u2)): t = n/2 + r with |r| <= 1/4
+// exactly, Taylor kernels in x = pi r (|x| <= pi/4; sin to x^17, cos to x^18: truncation < 1e-19), the quadrant
+// by n mod 4. Within 2e-16 of the exact sin/cos(2 pi u2) (20 M draws against long double; the library's
+// sincospi before it the same, the oracle's libm on the rounded 2 pi u2 7e-16). Written out so that its
+// coefficients are materialised where used (kc), not hoisted out of the step loop and spilled (the library
+// routine's were: 20 spilled VGPRs in the C4 kernel)
+__device__ __forceinline__ void sincospi_unit(double t, double& sn, double& cs) {
+    const double n = rint(2.0 * t);
+    const double r = fma(-0.5, n, t);   // exact
+    const double x = r * KC(3.141592653589793), z = x * x;
+    double ps = KC(2.8114572543455206e-15);
+    ps = fma(ps, z, KC(-7.647163731819816e-13));
+    ps = fma(ps, z, KC(1.6059043836821613e-10));
+    ps = fma(ps, z, KC(-2.505210838544172e-08));
+    ps = fma(ps, z, KC(2.7557319223985893e-06));
+    ps = fma(ps, z, KC(-0.0001984126984126984));
+    ps = fma(ps, z, KC(0.008333333333333333));
+    ps = fma(ps, z, KC(-0.16666666666666666));
+    const double S = fma(x * z, ps, x);
+    double pc = KC(-1.5619206968586225e-16);
+    pc = fma(pc, z, KC(4.779477332387385e-14));
+    pc = fma(pc, z, KC(-1.1470745597729725e-11));
+    pc = fma(pc, z, KC(2.08767569878681e-09));
+    pc = fma(pc, z, KC(-2.755731922398589e-07));
+    pc = fma(pc, z, KC(2.48015873015873e-05));
+    pc = fma(pc, z, KC(-0.001388888888888889));
+    pc = fma(pc, z, KC(0.041666666666666664));
+    const double C = fma(z * z, pc, fma(-0.5, z, 1.0));
+    const int q = (int)n & 3;
+    sn = q == 0 ? S : (q == 1 ? C : (q == 2 ? -S : -C));
+    cs = q == 0 ? C : (q == 1 ? -S : (q == 2 ? -C : S));
 }
 
 __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ctr, uint32_t tag, double& r0,
@@ -656,11 +714,15 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
     const double u1 = ((double)a + 0.5) * 0x1.0p-53;
     const double u2 = ((double)b + 0.5) * 0x1.0p-53;
     const double rad = sqrt(-2.0 * log_unit(u1));
-    // sin/cos(2 pi u2) as sincospi(2 u2): exact argument reduction without the large-argument
+    // sin/cos(2 pi u2) as sin/cos(pi (2 u2)): exact argument reduction without the large-argument
     // (Payne-Hanek) path, so the rare noise refill stays small in registers; agrees with the oracle's
-    // libm sin/cos(2 pi u2) to ~1 ulp (the oracle rounds 2 pi u2 first)
+    // libm sin/cos(2 pi u2) to < 1e-15 (the oracle rounds 2 pi u2 first)
     double s, co;
+#if QCART_SINCOS_OWN
+    sincospi_unit(2.0 * u2, s, co);
+#else
     sincospi(2.0 * u2, &s, &co);
+#endif
     r0 = rad * co;
     r1 = rad * s;
 }
@@ -1350,6 +1412,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // step loop, below.)
     constexpr bool HC = FAM != 2;
     const uint32_t genv = (uint32_t)(a.env_offset + env);
+    // the noise of the next 64 steps (lane j: step k + j): in the wave's LDS buffer (NZL) or in two registers
+    constexpr bool NZL = MODE >= 1 && sizeof(RT) == 8 && QCART_NZ_LDS;
     double nz0 = 0.0, nz1 = 0.0;
 
     int n_my = a.n_steps;
@@ -1391,17 +1455,32 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                  b4r = (RT)(HC ? a.b4 : a.a4 / a.a5);
         QC_STAMP(0);
         if ((k & 63) == 0) {   // lane j: normals of step k + j
+            double z0 = 0.0, z1 = 0.0;
             if (a.noise) {
                 const int kk = k + lane;
                 if (kk < n_my) {
-                    nz0 = a.noise[((size_t)kk * a.B + env) * 2];
-                    nz1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
+                    z0 = a.noise[((size_t)kk * a.B + env) * 2];
+                    z1 = a.noise[((size_t)kk * a.B + env) * 2 + 1];
                 }
             } else {
-                normals(a.seed, genv, ctr0 + (uint64_t)(k + lane), 0u, nz0, nz1);
+                normals(a.seed, genv, ctr0 + (uint64_t)(k + lane), 0u, z0, z1);
+            }
+            if constexpr (NZL) {
+                *(double2*)(simg0 + a.lds_nz + ei * kNzLds + lane * 16) = make_double2(z0, z1);
+            } else {
+                nz0 = z0;
+                nz1 = z1;
             }
         }
-        const double r0 = readlane_d(nz0, k & 63), r1 = readlane_d(nz1, k & 63);
+        double r0, r1;
+        if constexpr (NZL) {   // step k's pair: one broadcast read of the wave's buffer
+            const double2 z = *(const double2*)(simg0 + a.lds_nz + ei * kNzLds + (k & 63) * 16);
+            r0 = readlane_d(z.x, 0);
+            r1 = readlane_d(z.y, 0);
+        } else {
+            r0 = readlane_d(nz0, k & 63);
+            r1 = readlane_d(nz1, k & 63);
+        }
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = (HC ? a.k_dz : sdt * dt * 0.5) * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
         if (lane == 0) {
@@ -2261,7 +2340,8 @@ constexpr uint32_t kDualImg =
     slot_layout(Fam<FAM>::KL, R, FAM == 1, (uint32_t)sizeof(cx<RT>), slot_sym(FAM != 2, (uint32_t)sizeof(cx<RT>), 64), 64).tf +
     (FAM <= 1 ? (uint32_t)(R + 1 + (FAM == 1 ? R : 0)) * 64u * 8u : 0u);
 template <int FAM, int R, typename RT>
-constexpr bool kDual = sizeof(RT) == 8 && !(FAM == 2 && grid_rows_in_lds(R)) && 2u * ((kDualImg<FAM, R, RT> + 15u) & ~15u) <= 160u * 1024u;
+constexpr bool kDual = sizeof(RT) == 8 && !(FAM == 2 && grid_rows_in_lds(R)) &&
+                      2u * ((kDualImg<FAM, R, RT> + 15u) & ~15u) + (uint32_t)kStepWaves<FAM, R, RT> * kNzLds <= 160u * 1024u;
 
 // MODE 4 (the tables + the forward scan composites in LDS, the backward composites from L2) is instantiated for
 // the kernels whose MODE 2 image does not fit beside the grid row constants: the R = 17 grid kernel (C3)

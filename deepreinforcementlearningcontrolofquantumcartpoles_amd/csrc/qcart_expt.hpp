@@ -40,15 +40,6 @@
 #ifndef QCART_NZ_LDS
 #define QCART_NZ_LDS 1
 #endif
-// noise refill: its polynomial constants defined in place by VGPR (2) or SGPR (1; miscompiles the grid R = 17
-// MODE 0 kernel) asm, or plain literals (0: hoisted and spilled); the own sin/cos(pi t) (1) or the library
-// sincospi (0)
-#ifndef QCART_KC
-#define QCART_KC 2
-#endif
-#ifndef QCART_SINCOS_OWN
-#define QCART_SINCOS_OWN 1
-#endif
 // step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
 // R = 17 (C3) / fp32 R = 32 (C5) kernels
 #ifndef QCART_KAR_G17

@@ -634,26 +634,17 @@ __device__ __forceinline__ void philox10(uint32_t c[4], uint32_t k0, uint32_t k1
 // KC(x): the fp64 constant x defined where it is used, by an asm statement with no inputs that writes its two
 // halves (v_mov_b32 x 2), so nothing of it is loop-invariant to the optimiser. Written as plain literals, the
 // noise refill's polynomial constants were hoisted to the kernel entry, and the kernels at their register limit
-// spilled them (C4: 108 B of scratch per lane, ~0.1 GB of HBM traffic per launch). The SGPR form (QCART_KC = 1:
-// s_mov_b32 pairs, or a tied "+s" operand on the literal) miscompiles the R = 17 grid kernel's MODE 0
+// spilled them (C4: 108 B of scratch per lane, ~0.1 GB of HBM traffic per launch). The SGPR form of the same
+// (s_mov_b32 pairs, or a tied "+s" operand on the literal) miscompiled the R = 17 grid kernel's MODE 0
 // instantiation at its 106-SGPR limit — halves of the constants reloaded from the wrong SGPR-spill lanes, NaN in
 // test_table_placements_bitwise_equal[qo1025] — so the halves go through VGPRs (a few VALU moves per 64 steps).
 constexpr uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
 template <uint64_t B>
 __device__ __forceinline__ double kc_bits() {
-#if QCART_KC == 0
-    return __builtin_bit_cast(double, B);
-#else
     uint32_t lo, hi;
-#if QCART_KC == 2
     asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((int32_t)(uint32_t)B),
                  "i"((int32_t)(uint32_t)(B >> 32)));
-#else
-    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi) : "i"((int32_t)(uint32_t)B),
-                 "i"((int32_t)(uint32_t)(B >> 32)));
-#endif
     return __hiloint2double((int)hi, (int)lo);
-#endif
 }
 #define KC(x) kc_bits<dbits(x)>()
 __device__ __forceinline__ double log_unit(double x) {
@@ -718,11 +709,7 @@ __device__ __forceinline__ void normals(uint64_t seed, uint32_t env, uint64_t ct
     // (Payne-Hanek) path, so the rare noise refill stays small in registers; agrees with the oracle's
     // libm sin/cos(2 pi u2) to < 1e-15 (the oracle rounds 2 pi u2 first)
     double s, co;
-#if QCART_SINCOS_OWN
     sincospi_unit(2.0 * u2, s, co);
-#else
-    sincospi(2.0 * u2, &s, &co);
-#endif
     r0 = rad * co;
     r1 = rad * s;
 }

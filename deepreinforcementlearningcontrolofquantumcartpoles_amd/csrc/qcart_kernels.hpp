@@ -729,11 +729,13 @@ struct Tab {
     int vc, vr;    // this lane's byte offset in a complex / real lane-interleaved run
     int hc, hr;    // the same + 64 KiB (opaque): LDS images beyond the 16-bit ds_read offset field are
                    // addressed from this second base with immediate offsets instead of one add per read
+    int h2c, h2r;  // + 128 KiB (opaque where the image reaches past 128 KiB: C5's 160 KiB MODE 1 image, the grid's
+                   // MODE 2 / 4 images; 128 m2 / composite reads per C5 step each paid a v_add without it)
     __device__ __forceinline__ const char* atc(uint32_t off) const {
-        return off < 65536u ? lds + vc + off : lds + hc + (off - 65536u);
+        return off < 65536u ? lds + vc + off : (off < 131072u ? lds + hc + (off - 65536u) : lds + h2c + (off - 131072u));
     }
     __device__ __forceinline__ const char* atr(uint32_t off) const {
-        return off < 65536u ? lds + vr + off : lds + hr + (off - 65536u);
+        return off < 65536u ? lds + vr + off : (off < 131072u ? lds + hr + (off - 65536u) : lds + h2r + (off - 131072u));
     }
     __device__ __forceinline__ static cx<RT> lds_c(const char* p) {
         if constexpr (sizeof(RT) == 8) {
@@ -1231,6 +1233,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     constexpr bool SYMT = slot_sym(FAM != 2, (uint32_t)sizeof(cx<RT>), LE);   // L D L^T tables (no uc band)
     constexpr SlotLayout SL = slot_layout(KL, R, FAM == 1, sizeof(cx<RT>), SYMT, LE);
     constexpr uint32_t CE = (uint32_t)LE * sizeof(cx<RT>), CR = (uint32_t)LE * sizeof(RT);   // lane-run bytes
+    // end of the LDS table image at compile time (MODE 2: the kept levels and prefixes of both directions; MODE 4:
+    // the forward ones; MODE 1: the bands): reads past 128 KiB use Tab's third base
+    constexpr uint32_t NLI = (uint32_t)mode2_levels(KL), CBI = (uint32_t)(KL * KL) * CE;
+    constexpr uint32_t IMG_END = MODE == 2 ? SL.tf + (2u * NLI + 2u) * CBI : (MODE == 4 ? SL.tf + (NLI + 1u) * CBI : SL.tf);
+    constexpr bool T2 = (MODE == 1 || MODE == 2 || MODE == 4) && IMG_END > 131072u;
     const int lane = threadIdx.x & 63;
     const int gl = lane;   // lane of the env
     // env of this wave: order (envs grouped by force slot, EPB per block, -1 = idle) or identity
@@ -1477,9 +1484,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         // opaque per-step copy of the lane id for table addressing: keeps the loop-invariant table
         // reads and their addresses inside the step (LICM would otherwise pin them in registers)
         constexpr int EC = (int)sizeof(cx<RT>), ER = (int)sizeof(RT);
-        int lane_o = gl, hc = gl * EC + 65536, hr = gl * ER + 65536;
+        int lane_o = gl, hc = gl * EC + 65536, hr = gl * ER + 65536, h2c = gl * EC + 131072, h2r = gl * ER + 131072;
         asm volatile("" : "+v"(lane_o), "+v"(hc), "+v"(hr));
-        const Tab<MODE, RT> tb{rs, (const char*)simg, lane_o * EC, lane_o * ER, hc, hr};
+        if constexpr (T2) asm volatile("" : "+v"(h2c), "+v"(h2r));
+        const Tab<MODE, RT> tb{rs, (const char*)simg, lane_o * EC, lane_o * ER, hc, hr, h2c, h2r};
         double c1, c2, c3, c4, c5, c6;
         if constexpr (HC) {
             c1 = a.k_hisdt * dZ, c2 = a.k_qdt, c3 = a.k_qisdt * (dW * dW - dt);

@@ -1,9 +1,10 @@
 // Host check of the step kernel's sin/cos(pi t) (qcart_kernels.hpp sincospi_unit, same operations in C with
 // fma/rint): 2e7 Box-Muller angles t = 2 u2 against long double, and libm on the rounded 2 pi u2 beside it.
-//   gcc -O2 -o /tmp/sincospi_check tools/sincospi_check.c -lm && /tmp/sincospi_check
+//   gcc -O2 -o /tmp/sincospi_check tools/sincospi_check.c -lm && /tmp/sincospi_check [draws]
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 static void scp(double t, double* s, double* c) {
     const double n = rint(2.0 * t);
     const double r = fma(-0.5, n, t);
@@ -30,9 +31,10 @@ static void scp(double t, double* s, double* c) {
     *s = q == 0 ? S : q == 1 ? C : q == 2 ? -S : -C;
     *c = q == 0 ? C : q == 1 ? -S : q == 2 ? -C : S;
 }
-int main() {
+int main(int argc, char** argv) {
+    const long n = argc > 1 ? atol(argv[1]) : 20000000;
     uint64_t st = 88172645463325252ull; double ms = 0, mc = 0, msr = 0;
-    for (long i = 0; i < 20000000; ++i) {
+    for (long i = 0; i < n; ++i) {
         st ^= st << 13; st ^= st >> 7; st ^= st << 17;
         const double u2 = ((double)(st >> 11) + 0.5) * 0x1.0p-53;
         double s, c; scp(2.0 * u2, &s, &c);

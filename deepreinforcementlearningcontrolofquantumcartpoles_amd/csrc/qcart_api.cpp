@@ -213,7 +213,7 @@ KArgs base_args(const qc_handle* h) {
     a.Npad = op.Npad;
     a.n_slots = (int32_t)h->acts.size();
     a.mirror = h->mirror ? 1 : 0;
-    a.bnd_len = op.fock ? 5 : 6;
+    a.bnd_len = op.fock ? kFockBnd : kGridBnd;
     a.win_lo = a.win_hi = 0;
     if (!op.fock && p.xth > 0) {
         const int c = op.N / 2, w = (int)std::nearbyint(p.xth / op.h);   // IQO/main_parallel.py:78-81
@@ -322,8 +322,9 @@ int validate_params(const qc_params* p, std::string& err) {
         err = "n_actions must be odd and <= 64";
         return QC_EINVAL;
     }
-    if (p->family >= QC_QO && (p->moment_order < 1 || p->moment_order > 6)) {
-        err = "moment_order must be in 1..6";
+    if (p->family >= QC_QO && (p->moment_order < 1 || p->moment_order > kMaxMomentOrder)) {
+        // one observable per lane of the env's wave: (2 + m + 1) m / 2 <= 64
+        err = "moment_order must be in 1..9 (the (2+m+1)*m/2 observables, one per lane of a 64-lane wave)";
         return QC_EINVAL;
     }
     if (p->a_mode != QC_A_REFERENCE && p->a_mode != QC_A_EXACT) { err = "bad a_mode"; return QC_EINVAL; }
@@ -563,6 +564,9 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.fail_step = fail_step;
     a.term_step = term_step;
     a.obs_out = obs_out;
+    // grid moment orders above the step kernel's fused epilogue: the observation kernel runs after the step
+    const bool obs_after = obs_out && !h->op.fock && h->p.moment_order > kStepMaxMomentOrder;
+    if (obs_after) a.obs_out = nullptr;
     DeviceGuard g(h->device);
     if (h->p.batch == 0) return QC_OK;
     if (!noise && h->noise_mode == QC_NOISE_MT19937 && n_steps > 0) {
@@ -629,6 +633,13 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     int rc = launch_step(h->p.family, h->op.Rs, a, h->stream);
     if (h->timing) (void)hipEventRecord(ev1, h->stream);
     if (rc) return fail(h, rc, rc == QC_ENOTBUILT ? "kernel not built" : "step kernel launch failed");
+    if (obs_after) {
+        KArgs o = base_args(h);
+        o.psi = (double*)psi;
+        o.obs_out = obs_out;
+        rc = launch_obs(h->p.family, h->R, o, h->stream);
+        if (rc) return fail(h, rc, "obs kernel launch failed");
+    }
     return QC_OK;
 }
 

@@ -26,27 +26,10 @@
 #ifndef QCART_SPLITM
 #define QCART_SPLITM 1
 #endif
-// step kernel: the fp32 R = 32 kernel recomputes rel after the Horner (1) or holds it through (0)
-#ifndef QCART_RECREL
-#define QCART_RECREL 0
-#endif
-// step kernel: the fp32 mirror update as packed v_pk_fma (1: C5 -0.6 %, but 17 spilled registers whose scratch
-// footprint adds 0.11 GB of HBM writes per launch) or scalar FMAs (0: no spills, psi once out)
-#ifndef QCART_PKMIR
-#define QCART_PKMIR 0
-#endif
 // step kernel: the 64-step noise refill parked in a 1 KiB per-wave LDS buffer, read back one step at a time (1), or
 // held in 4 VGPRs across the step loop (0) — fp64 kernels with LDS tables (MODE >= 1)
 #ifndef QCART_NZ_LDS
 #define QCART_NZ_LDS 1
-#endif
-// step kernel: re-read the loop's uniform constants from the kernarg segment every step (KAR) also in the grid
-// R = 17 (C3) / fp32 R = 32 (C5) kernels
-#ifndef QCART_KAR_G17
-#define QCART_KAR_G17 0
-#endif
-#ifndef QCART_KAR_F32
-#define QCART_KAR_F32 0
 #endif
 // measurement actor (qcart_actor.hip): conv1..3 column tiles per wave, accumulator sets, k-steps per load batch;
 // fc1 output tiles x env tiles per wave

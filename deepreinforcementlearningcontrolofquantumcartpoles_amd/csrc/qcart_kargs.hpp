@@ -50,6 +50,18 @@ constexpr bool grid_rows_in_lds(int R) { return R >= 17; }
 // bytes of LDS per wave for the step loop's noise refill (64 steps x 2 normals): fp64 kernels with LDS tables
 constexpr uint32_t kNzLds = 1024;
 
+// boundary bands of check_boundary_error: the top kFockBnd Fock levels (IHO/simulation_i.cpp:422-426,
+// HO/simulation.cpp:403-407), kGridBnd points at either end of the grid (QO/simulation_quart.cpp:559-565). The
+// grid step kernel's normalise is specialised on kGridBnd at compile time (qcart_kernels.hpp)
+constexpr int kFockBnd = 5;
+// highest grid moment order (get_moments' MOMENT, QO/setupC.py:16,38): the observation kernel holds observable i in
+// lane i of the env's wave, (2 + m + 1) m / 2 <= 64 (m = 9: 54 observables; m = 10 would need 65)
+constexpr int kMaxMomentOrder = 9;
+// the step kernel's fused observation epilogue covers orders up to this one (qc_step runs the observation kernel
+// after the step for higher orders)
+constexpr int kStepMaxMomentOrder = 6;
+constexpr int kGridBnd = 6;
+
 struct KArgs {
     // state and I/O (device pointers)
     void* psi;                 // [B][N] complex interleaved, fp64 or fp32 (precision)
@@ -71,7 +83,7 @@ struct KArgs {
     int32_t default_action;
     int32_t n_slots;
     int32_t mirror;            // IHO reference-mode Hermitian mirror correction
-    int32_t bnd_len;           // 5 (Fock) or 6 (grid)
+    int32_t bnd_len;           // kFockBnd (Fock) or kGridBnd (grid)
     int32_t win_lo, win_hi;    // IQO outside-probability window [lo, hi); win_hi <= win_lo: off
     int32_t moment_order;
     int32_t n_obs;

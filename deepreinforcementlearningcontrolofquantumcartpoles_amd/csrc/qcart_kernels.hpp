@@ -488,6 +488,18 @@ struct RowReg {
     __device__ __forceinline__ double h(int j) const { return hd[j]; }
     __device__ __forceinline__ double x(int j) const { return xg[j]; }
 };
+// RowGlb: the MODE 0 fallback of the R = 17 kernel (its image does not fit, or QCART_TAB_MODE=0) reads them from the
+// handle's operator rows in global memory (cached), hfd formed per use by the same expression as RowReg / the LDS
+// image fill; held in registers (RowReg) they spilled that instantiation (22 spilled VGPRs, 68 B of scratch)
+template <int R>
+struct RowGlb {
+    const double* hu;
+    const double* xg;
+    double cF;
+    int base;
+    __device__ __forceinline__ double h(int j) const { return hu[base + j] - cF * xg[base + j]; }
+    __device__ __forceinline__ double x(int j) const { return xg[base + j]; }
+};
 template <int R>
 struct RowLds {
     const char* p;
@@ -1114,8 +1126,12 @@ __device__ __forceinline__ void grid_p(const cd (&v)[R], cd (&o)[R], double pbar
     }
 }
 
-constexpr int kMaxMoment = 6;                 // obs vector up to (2+6+1)*6/2 = 27
-constexpr int kMaxObs = (2 + kMaxMoment + 1) * kMaxMoment / 2;
+// moment orders: the standalone observation kernel (k_obs) computes up to kMaxMoment (one lane per observable:
+// (2+9+1)*9/2 = 54 of the wave's 64 lanes), the step kernel's fused epilogue up to kStepMaxMoment (the drivers'
+// default 5; its p-power passes are unrolled into the step kernel, whose registers the higher orders would cost) —
+// qc_step runs k_obs after the step for orders above it (qcart_api.cpp)
+constexpr int kMaxMoment = kMaxMomentOrder;
+constexpr int kStepMaxMoment = kStepMaxMomentOrder;
 
 // compute_statistics (QO/simulation_quart.cpp:326-362). Returns this lane's entry of the observation vector
 // (lane 0 <x>, lane 1 <p>, lane i >= 2 the centred moment i; lanes >= n_obs: unused): the moments of one p-power b
@@ -1127,10 +1143,10 @@ constexpr int kMaxObs = (2 + kMaxMoment + 1) * kMaxMoment / 2;
 // psi's registers — the scheduler batches the re-reads, 156 -> 216 spilled registers)
 // XM(): an accessor of the rows' x_r (.x(j)) — cf.xg, or (R = 17 step kernel) the block's LDS row constants, made
 // fresh per pass so that the 2 R registers of x are not held across the passes
-template <int B, int R, typename PS, typename XM>
+template <int MM, int B, int R, typename PS, typename XM>
 __device__ __forceinline__ void grid_obs_pow(const PS& ps, const XM& xm, cd (&v)[R], const Coef<2, R>& cf, int lane,
                                              int m, double xbar, double pbar, double inv_h, double h, double& ov) {
-    if constexpr (B <= kMaxMoment) {
+    if constexpr (B <= MM) {
         if (B > m) return;
         if constexpr (B > 0) {
             cd nv[R];
@@ -1138,7 +1154,7 @@ __device__ __forceinline__ void grid_obs_pow(const PS& ps, const XM& xm, cd (&v)
 #pragma unroll
             for (int j = 0; j < R; ++j) v[j] = nv[j];
         }
-        constexpr int A0 = B >= 2 ? 0 : 2 - B, A1 = kMaxMoment - B, NA = A1 - A0 + 1;
+        constexpr int A0 = B >= 2 ? 0 : 2 - B, A1 = MM - B, NA = A1 - A0 + 1;
         double acc[NA];
 #pragma unroll
         for (int i = 0; i < NA; ++i) acc[i] = 0.0;
@@ -1161,11 +1177,11 @@ __device__ __forceinline__ void grid_obs_pow(const PS& ps, const XM& xm, cd (&v)
             const int jj = aa + B, idx = 2 + (jj - 2) * (jj + 3) / 2 + B;
             ov = lane == idx ? acc[aa - A0] * h : ov;
         }
-        grid_obs_pow<B + 1, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+        grid_obs_pow<MM, B + 1, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
     }
 }
 
-template <int R, typename XM>
+template <int MM, int R, typename XM>
 __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>& cf, const XM& xm, int lane, int m,
                                            double h) {
     const double inv_h = 1.0 / h;
@@ -1184,7 +1200,7 @@ __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>&
 #pragma unroll
     for (int j = 0; j < R; ++j) v[j] = psi[j];
     auto ps = [&](int j) -> cd { return psi[j]; };
-    grid_obs_pow<0, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+    grid_obs_pow<MM, 0, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
     return ov;
 }
 
@@ -1369,8 +1385,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // grid: H_F's diagonal with the slot's force folded in, once per call (MODE 0: registers; MODE >= 1:
     // the block's LDS image, RowLds)
     constexpr bool RCL = FAM == 2 && MODE >= 1 && grid_rows_in_lds(R);
-    RT hfd[FAM == 2 && !RCL ? R : 1];
-    if constexpr (FAM == 2 && !RCL) {
+    constexpr bool RGL = FAM == 2 && MODE == 0 && grid_rows_in_lds(R);
+    RT hfd[FAM == 2 && !RCL && !RGL ? R : 1];
+    if constexpr (FAM == 2 && !RCL && !RGL) {
 #pragma unroll
         for (int j = 0; j < R; ++j) hfd[j] = cf.hu[j] - cF * cf.xg[j];
     }
@@ -1379,6 +1396,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             int vo = lane * 8;
             asm volatile("" : "+v"(vo));
             return RowLds<R>{(const char*)simg + a.lds_fx, vo};
+        } else if constexpr (RGL) {
+            int bo = base;
+            asm volatile("" : "+v"(bo));
+            return RowGlb<R>{a.hu, a.xg, cFd, bo};
         } else if constexpr (FAM == 2) {
             return RowReg<R>{hfd, cf.xg};
         } else {
@@ -1419,7 +1440,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
-    constexpr bool KAR = (!(FAM == 2 && R >= 17) || QCART_KAR_G17) && (!(sizeof(RT) == 4 && R >= 32) || QCART_KAR_F32);
+    constexpr bool KAR = !(FAM == 2 && R >= 17) && !(sizeof(RT) == 4 && R >= 32);
     // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
     // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
@@ -1461,6 +1482,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             }
             if constexpr (NZL) {
                 *(double2*)(simg0 + a.lds_nz + ei * kNzLds + lane * 16) = make_double2(z0, z1);
+                // every lane's pair is read by the whole wave below: order the wave's stores before those reads
+                // explicitly (a wave's LDS accesses issue in order; this keeps the compiler from moving them)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
             } else {
                 nz0 = z0;
                 nz1 = z1;
@@ -1627,7 +1652,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 // boundary bands and the window edges are suffix sums captured at (wave-uniform) rows, by an FMA with
                 // a 0 / 1 weight (no per-row lane predicates), the lanes between them add whole. One reduction for
                 // the norm, <x> and the window (QO reduces a zero).
-                constexpr int BND = 6;                            // the grid's boundary band (a.bnd_len)
+                constexpr int BND = kGridBnd;                     // the grid's boundary band (= a.bnd_len)
                 constexpr int LB = (BND - 1) / R, JB = BND - LB * R;   // bottom band: lanes < LB whole, lane LB rows < JB
                 const int r0 = N - BND, lt = r0 / R, jt = r0 - lt * R;
                 const int wl = a.win_lo < 0 ? 0 : a.win_lo, wh = a.win_hi > 64 * R ? 64 * R : a.win_hi;
@@ -1688,9 +1713,6 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         //   C  acc = psi + kA rel + k2 D1 + u + mirror(D1);  psi <- Y0 = psi + dt D1
         //   D  Y- branch, then Y+ branch (D1ImRe IHO:301-318, D2 IHO:320-333)
         //   E  Phi+- means from <Y+, X rel+> products (no X Phi+- applications)
-        // RECREL (the fp32 R = 32 kernel): rel is recomputed after the Horner instead of held through it (one
-        // more X application, 64 VGPRs fewer live in the term7 phase; QCART_RECREL)
-        constexpr bool RECREL = sizeof(RT) == 4 && R >= 32 && QCART_RECREL;
         cx<RT> acc[R], rel[R], D1[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) rel[j] = C(xp[j].re - xbar * psi[j].re, xp[j].im - xbar * psi[j].im);
@@ -1726,11 +1748,6 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
             for (int j = 0; j < R; ++j) t[j] = C(acc[j].re + b2r * D1[j].re, acc[j].im + b2r * D1[j].im);
             hf(t, acc);
             hf(acc, t);
-            if constexpr (RECREL) {   // rel = (X - xbar) psi again (psi not yet updated): not held through the Horner
-                apply_x<FAM, R>(psi, rel, cf, lnv);
-#pragma unroll
-                for (int j = 0; j < R; ++j) rel[j] = C(rel[j].re - xbar * psi[j].re, rel[j].im - xbar * psi[j].im);
-            }
             const RT kA = (RT)((dW - 2.0 * c4) * beta), k2 = (RT)(2.0 * c2);
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -1762,11 +1779,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                             const int d = MB * h + dd + 1;
                             const cx<RT> dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
                                                        : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
-                            if constexpr (kPk<RT> && QCART_PKMIR) {   // acc + m (-i dv): one v_pk_fma (op_sel swap, neg_hi)
-                                acc[j] = CV(__builtin_elementwise_fma((v2f){mv[dd][j], -mv[dd][j]}, dv.v.yx, acc[j].v));
-                            } else {
-                                acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
-                            }
+                            acc[j] = C(acc[j].re + mv[dd][j] * dv.im, acc[j].im - mv[dd][j] * dv.re);
                         }
                 }
             }
@@ -2041,7 +2054,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                 a.obs_out[(size_t)env * 5 + lane] = v;
             }
         } else {
-            const double v = grid_obs<R>(psi, cf, rowc, lane, a.moment_order, a.h);
+            const double v = grid_obs<kStepMaxMoment, R>(psi, cf, rowc, lane, a.moment_order, a.h);
             if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
         }
     }
@@ -2101,7 +2114,7 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
         }
     } else {
         auto xm = [&]() { return RowReg<R>{cf.xg, cf.xg}; };
-        const double v = grid_obs<R>(psi, cf, xm, lane, a.moment_order, a.h);
+        const double v = grid_obs<kMaxMoment, R>(psi, cf, xm, lane, a.moment_order, a.h);
         if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
     }
 }

@@ -39,7 +39,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU test")
     # only the controlling process of a session (pytest-xdist workers carry `workerinput`: each would start a
     # child of its own)
-    if _selects_gpu(config) and os.path.exists("/dev/kfd") and not hasattr(config, "workerinput"):
+    # with -n (pytest-xdist) the controller never runs pytest_collection_modifyitems (the workers collect), so
+    # the child could not be ordered alone before the GPU tests: no child then (test_gpu_rccl skips on the
+    # workers); the GPU suite is run without -n
+    dist = config.getoption("dist", "no") if hasattr(config.option, "dist") else "no"
+    nproc = getattr(config.option, "numprocesses", None)
+    if (_selects_gpu(config) and os.path.exists("/dev/kfd") and not hasattr(config, "workerinput")
+            and dist == "no" and not nproc):
         _start_rccl_child(config)
 
 

@@ -258,6 +258,29 @@ def test_moments_parity(oracle_mod, name):
     np.testing.assert_allclose(out["obs"].cpu().numpy(), got, rtol=5e-16, atol=1e-15)
 
 
+@pytest.mark.parametrize("order", [1, 7, 9])
+def test_high_moment_orders_match_oracle(oracle_mod, order):
+    """get_moments beyond the drivers' default order (QO/setupC.py compiles any MOMENT >= 1;
+    QO/simulation_quart.cpp:326-388): orders above the step kernel's fused epilogue (6) run the observation
+    kernel after the step; up to 9 ((2+9+1)*9/2 = 54 observables, one per lane); 10 is refused."""
+    ph = CASES["qo171"].with_(moment_order=order)
+    B = 3
+    osys = oracle_sys(oracle_mod, ph)
+    psi0 = init_states(osys, ph, B, seed=5)
+    osys.run_batch(psi0, np.full(B, 14, np.int32), ph.f_max, 30, ph.dt, ph.gamma, seed=2, n_threads=4)
+    st = Stepper(ph, B, 0)
+    assert st.n_obs == (2 + order + 1) * order // 2
+    psi = torch.from_numpy(psi0.copy()).cuda()
+    got = st.moments(psi).cpu().numpy()
+    ref = np.stack([osys.moments(p) for p in psi0])
+    assert ref.shape == got.shape
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-11)
+    out = st.step(psi, None, 0, want_obs=True)   # the step call's observation (fused or after the step)
+    np.testing.assert_allclose(out["obs"].cpu().numpy(), got, rtol=5e-16, atol=1e-15)
+    with pytest.raises(Exception):
+        Stepper(ph.with_(moment_order=10), B, 0)
+
+
 def test_outside_probability_and_term_step(oracle_mod):
     ph = CASES["iqo513"]
     B = 3

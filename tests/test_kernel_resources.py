@@ -1,0 +1,88 @@
+"""Register / spill / scratch budgets of every shipped step-kernel instantiation, read on the CPU from the code
+objects inside the built libqcart.so (tools/kernel_resources.py: the .hip_fatbin bundles' metadata notes).
+
+A spill regression is silent otherwise: a compiler or code-shape change that makes a step kernel spill costs
+scratch traffic every step (round 2: 1.1 GB of HBM writes per metric launch), and round 4's NaN came from an
+instantiation at its SGPR limit reloading constants from the wrong spill lanes. Budgets:
+  * every k_step instantiation: no VGPR spills and no scratch, except the documented ones below;
+  * two waves per SIMD (8-env workgroups): at most 256 VGPRs (the metric's k_step<1,8,*,double>, C4's grid R = 9,
+    C2, the fp32 R <= 16 kernels);
+  * one wave per SIMD: at most 512 VGPRs (C3's grid R = 17, C5's fp32 R = 32, IHO fp64 R = 16).
+"""
+import os
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "deepreinforcementlearningcontrolofquantumcartpoles_amd", "libqcart.so")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+STEP = re.compile(r"k_stepILi(\d+)ELi(\d+)ELi(\d+)E([df])Lb([01])E")
+
+# (family, R, MODE, RT, DUAL) -> (max VGPR spills, max scratch bytes): the documented exceptions. The metric's two-slot
+# body (DUAL, MODE 2 and its MODE 1 variant) keeps 2 spilled registers outside the step loop (12 B per lane, written
+# once per wave); the IHO fp64 R = 16 kernel (N <= 1024, one wave per SIMD) and the HO fp32 R = 32 kernel (N <= 2048)
+# spill a few registers into AGPR-free VGPR lanes (no scratch)
+EXCEPTIONS = {
+    (1, 8, 2, "d", 1): (2, 12),
+    (1, 8, 1, "d", 1): (2, 12),
+    (1, 16, 2, "d", 0): (8, 0),
+    (1, 16, 1, "d", 0): (8, 0),
+    (0, 32, 2, "f", 0): (8, 28),
+    (0, 32, 1, "f", 0): (8, 12),
+    (0, 32, 0, "f", 0): (8, 0),
+}
+
+
+def step_waves(fam, R, rt):
+    """kStepWaves (qcart_kernels.hpp): 8 waves (two per SIMD) where the step fits 256 VGPRs."""
+    r_eff = R * (4 if rt == "f" else 8) // 8
+    return 8 if ((fam <= 1 and r_eff <= 8) or (fam == 2 and R <= 9)) else 4
+
+
+@pytest.fixture(scope="module")
+def step_kernels():
+    if not os.path.exists(LIB):
+        pytest.skip("libqcart.so not built")
+    import kernel_resources as K
+    out = {}
+    for name, v, s, scr, sp in K.kernels(LIB):
+        m = STEP.search(name)
+        if m:
+            key = (int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4), int(m.group(5)))
+            out[key] = (int(v), int(s), int(scr), int(sp))
+    return out
+
+
+def test_every_config_kernel_is_present(step_kernels):
+    want = [(1, 8, 2, "d", 1),    # metric / C2 (two-slot launch)
+            (2, 17, 4, "d", 0),   # C3
+            (2, 9, 2, "d", 1),    # C4
+            (1, 32, 1, "f", 0),   # C5
+            (0, 4, 2, "d", 1)]    # C1 (HO N = 256)
+    for k in want:
+        assert k in step_kernels, k
+
+
+def test_step_kernels_do_not_spill(step_kernels):
+    bad = []
+    for k, (v, s, scr, sp) in sorted(step_kernels.items()):
+        max_sp, max_scr = EXCEPTIONS.get(k, (0, 0))
+        if sp > max_sp or scr > max_scr:
+            bad.append((k, sp, scr))
+    assert not bad, f"(family, R, MODE, RT, DUAL) with spills / scratch over budget: {bad}"
+
+
+def test_register_budget_matches_waves_per_simd(step_kernels):
+    for (fam, R, mode, rt, dual), (v, s, scr, sp) in step_kernels.items():
+        cap = 256 if step_waves(fam, R, rt) == 8 else 512
+        assert v <= cap, ((fam, R, mode, rt, dual), v, cap)
+        assert s <= 106, ((fam, R, mode, rt, dual), s)
+
+
+def test_metric_kernel_budget(step_kernels):
+    """The metric kernel (IHO N = 512, two waves per SIMD): <= 256 VGPRs, <= 12 B of scratch."""
+    v, s, scr, sp = step_kernels[(1, 8, 2, "d", 1)]
+    assert v <= 256 and scr <= 12 and sp <= 2

@@ -17,7 +17,12 @@ def executed_frac(prof, tag, c, bl):
     f = os.path.join(prof, f"{tag}_{c}_sq.json")
     if not os.path.exists(f):
         return None
-    d = json.load(open(f))["derived"]
+    sq = json.load(open(f))
+    # only a profile of this same library build and workload prices this bench line's kernel
+    if (sq.get("lib_sha") != bl["roofline"].get("lib_sha")
+            or sq.get("workload") != bl["config"].get("workload")):
+        return None
+    d = sq["derived"]
     fp32 = bl["dtype"] == "f32"
     fl = d.get("fp32_flops_counter_per_wave_step" if fp32 else "fp64_flops_counter_per_wave_step")
     if not fl:

@@ -88,7 +88,9 @@ def main():
             if k in per:
                 fl = per[k] / ws
                 der[f"{prec.lower()}_flops_counter_per_wave_step"] = fl
-                lines.append(f"#   {k} {fl:.0f} per wave-step = {fl / N:.1f} per row")
+                # the counter sums each wave instruction's flops of ONE lane (an FMA 2, a v_pk_fma_f32 4): x 64 lanes
+                # per wave-step, / N rows
+                lines.append(f"#   {k} {fl:.0f} per wave-step (one lane) = {64 * fl / N:.0f} flops per row")
         for k, lab in (("SQ_INSTS_VALU_INT32", "INT32 VALU"), ("SQ_INSTS_VALU_INT64", "INT64 VALU"),
                        ("SQ_INSTS_VALU_CVT", "CVT VALU"), ("SQ_INSTS_VALU_TRANS_F32", "TRANS F32"),
                        ("SQ_INSTS_VALU_TRANS_F64", "TRANS F64"), ("SQ_INSTS_LDS", "LDS instructions"),
@@ -104,6 +106,13 @@ def main():
             lines.append(f"#   shader clock                 {clk / 1e6:.0f} M cycles per XCD per launch")
             lines.append(f"#   VALU issue share             {der['valu_issue_share']:.2f}"
                          "  (INSTS_VALU x 4 cycles / (1024 SIMDs x clock))")
+            f64 = sum(g(f"SQ_INSTS_VALU_{k}_F64", 0) for k in ("FMA", "MUL", "ADD"))
+            if f64:
+                # a wave64 FP64 FMA occupies the SIMD 4 cycles (78.6 TF = 16 FMA / cycle / SIMD); a 32-bit op 2 cycles
+                # when two waves share the SIMD: the share of SIMD cycles the FP64 instructions alone fill
+                der["fp64_pipe_share"] = f64 * 4 / (1024 * clk)
+                lines.append(f"#   FP64 pipe share              {der['fp64_pipe_share']:.2f}"
+                             "  (FP64 FMA/MUL/ADD x 4 cycles / (1024 SIMDs x clock))")
         if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
             der["active_valu_per_wave_cycle"] = per["SQ_ACTIVE_INST_VALU"] / per["SQ_WAVE_CYCLES"]
             lines.append(f"#   ACTIVE_INST_VALU / WAVE_CYCLES {der['active_valu_per_wave_cycle']:.2f}")

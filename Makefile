@@ -8,10 +8,15 @@ LIB := $(PKG)/libqcart.so
 # arithmetic; an env's trajectory never depends on which workgroup shape it ran in (the backend's "fast"
 # contraction fused differently per instantiation)
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -ffp-contract=on
-OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o)
-HDRS := include/qcart.h $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp
+OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o qcart_server.o)
+HDRS := include/qcart.h $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp $(CSRC)/qcart_shm.h
+# the step server's client side: plain C (POSIX shared memory + futexes), no HIP
+CLIENT := $(PKG)/libqcart_client.so
 
-all: $(LIB) oracle
+all: $(LIB) $(CLIENT) oracle
+
+$(CLIENT): $(CSRC)/qcart_client.c $(CSRC)/qcart_shm.h include/qcart_client.h Makefile
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lrt
 
 # kernel TUs: MachineLICM off — it hoists loop-invariant FP64 constants of the step loop's rare
 # noise refill into registers that then spill (same speed, ~0.9 GB less scratch traffic per launch)
@@ -31,13 +36,13 @@ $(CSRC)/build/%.o: $(CSRC)/%.cpp $(HDRS) Makefile
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -lrt
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(CSRC)/build $(LIB)
+	rm -rf $(CSRC)/build $(LIB) $(CLIENT)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean resource-usage expt expt_actor

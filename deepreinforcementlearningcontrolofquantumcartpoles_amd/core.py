@@ -18,6 +18,31 @@ def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def make_params(physics: Physics, batch: int, seed: int = 42, env_offset: int = 0,
+                xth: float | None = None) -> L.QcParams:
+    """qc_params of a handle for `physics` (the setupC.py macros + the drivers' step() arguments)."""
+    p = L.QcParams()
+    p.family = physics.family
+    p.n_max = physics.n_max
+    p.omega = physics.omega
+    p.x_max = physics.x_max
+    p.grid_size = physics.grid_size
+    p.lambda_ = physics.lambda_
+    p.mass = physics.mass
+    p.moment_order = physics.moment_order
+    p.a_mode = physics.a_mode
+    p.precision = physics.precision
+    p.gamma = physics.gamma
+    p.dt = physics.dt
+    p.f_max = physics.f_max
+    p.n_actions = physics.n_actions
+    p.batch = int(batch)
+    p.env_offset = int(env_offset)
+    p.seed = seed
+    p.xth = physics.xth if (xth is None and physics.family == 3) else (xth or 0.0)
+    return p
+
+
 class Stepper:
     """B environments of one physical system on one device (one handle, one HIP stream)."""
 
@@ -31,25 +56,7 @@ class Stepper:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.env_offset = int(env_offset)
-        p = L.QcParams()
-        p.family = physics.family
-        p.n_max = physics.n_max
-        p.omega = physics.omega
-        p.x_max = physics.x_max
-        p.grid_size = physics.grid_size
-        p.lambda_ = physics.lambda_
-        p.mass = physics.mass
-        p.moment_order = physics.moment_order
-        p.a_mode = physics.a_mode
-        p.precision = physics.precision
-        p.gamma = physics.gamma
-        p.dt = physics.dt
-        p.f_max = physics.f_max
-        p.n_actions = physics.n_actions
-        p.batch = self.batch
-        p.env_offset = self.env_offset
-        p.seed = seed
-        p.xth = physics.xth if (xth is None and physics.family == 3) else (xth or 0.0)
+        p = make_params(physics, self.batch, seed, self.env_offset, xth)
         self._params = p
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):

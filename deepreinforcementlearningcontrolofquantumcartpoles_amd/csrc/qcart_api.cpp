@@ -480,20 +480,24 @@ int qc_env_counters(qc_handle* h, uint64_t* out, const uint64_t* in) {
         return QC_EHIP;
     return QC_OK;
 }
-int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds) {
+int qc_set_seed_mt19937_envs(qc_handle* h, const uint32_t* seeds, const uint8_t* mask) {
     if (!h) return QC_EINVAL;
     if (h->p.batch > 0 && !seeds) return fail(h, QC_EINVAL, "seeds is null");
+    if (mask && h->noise_mode != QC_NOISE_MT19937)
+        return fail(h, QC_EINVAL, "a masked reseed needs every env's MT19937 stream (qc_set_seed_mt19937 first)");
     DeviceGuard g(h->device);
     if (h->p.batch > 0) {
         if (!h->d_mt) {
             hipError_t e = hipMalloc((void**)&h->d_mt, (size_t)h->p.batch * kMtWords * sizeof(uint32_t));
             if (e != hipSuccess) { h->d_mt = nullptr; return fail(h, QC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
         }
-        if (launch_mt_seed(seeds, h->p.batch, h->d_mt, h->stream)) return fail(h, QC_EHIP, "MT19937 seed kernel launch failed");
+        if (launch_mt_seed(seeds, mask, h->p.batch, h->d_mt, h->stream))
+            return fail(h, QC_EHIP, "MT19937 seed kernel launch failed");
     }
     h->noise_mode = QC_NOISE_MT19937;
     return QC_OK;
 }
+int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds) { return qc_set_seed_mt19937_envs(h, seeds, nullptr); }
 int qc_noise_mode(const qc_handle* h) { return h ? h->noise_mode : QC_EINVAL; }
 int qc_mt19937_state(qc_handle* h, uint32_t* out, const uint32_t* in) {
     if (!h) return QC_EINVAL;

@@ -1,0 +1,229 @@
+/*
+ * qcart_client.c — libqcart_client.so: the actor-process side of the step server (qcart_server.cpp).
+ * Plain C over POSIX shared memory and futexes: no HIP, no GPU context in the client process (the reference's
+ * actors each own a CPU-only `simulation` module; here they own one slot of the server's batch).
+ * Protocol and layout: qcart_shm.h. A call copies the state into the slot's row, publishes req + 1, and waits
+ * (a short spin, then a futex on the header's tick word) until the server has published done = req.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../../include/qcart_client.h"
+#include "qcart_shm.h"
+
+struct qcc {
+    int fd;
+    size_t bytes;
+    unsigned char* shm;
+    qcs_header* hdr;
+    qcs_slot* slot;
+    double* psi;   /* this slot's state row [2N] */
+    double* obs;   /* this slot's observation row [QCS_MAX_OBS] */
+    int index;
+    char err[160];
+};
+
+static char g_err[160];
+
+static void set_err(qcc* c, const char* m) {
+    snprintf(c ? c->err : g_err, sizeof(g_err), "%s", m);
+}
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+int qcc_open(const char* name, qcc** out) {
+    if (!out || !name) return QCC_EINVAL;
+    *out = NULL;
+    int fd = shm_open(name, O_RDWR, 0);
+    if (fd < 0) {
+        snprintf(g_err, sizeof(g_err), "no step server at %s (shm_open: %s)", name, strerror(errno));
+        return QCC_ENOSERVER;
+    }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0 || (size_t)sb.st_size < sizeof(qcs_header)) {
+        close(fd);
+        snprintf(g_err, sizeof(g_err), "%s is not a step-server object", name);
+        return QCC_ENOSERVER;
+    }
+    unsigned char* m = (unsigned char*)mmap(NULL, (size_t)sb.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) {
+        close(fd);
+        snprintf(g_err, sizeof(g_err), "mmap: %s", strerror(errno));
+        return QCC_ENOSERVER;
+    }
+    qcs_header* h = (qcs_header*)m;
+    if (h->magic != QCS_MAGIC || h->version != QCS_VERSION || h->total_bytes != (uint64_t)sb.st_size ||
+        !__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) {
+        munmap(m, (size_t)sb.st_size);
+        close(fd);
+        snprintf(g_err, sizeof(g_err), "%s: no live step server (version / state mismatch)", name);
+        return QCC_ENOSERVER;
+    }
+    qcs_slot* slots = (qcs_slot*)(m + h->slot_off);
+    int idx = -1;
+    for (int e = 0; e < h->max_clients && idx < 0; ++e) {
+        uint32_t z = 0;
+        if (__atomic_compare_exchange_n(&slots[e].owner, &z, 1u, 0, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED)) idx = e;
+    }
+    if (idx < 0) {
+        snprintf(g_err, sizeof(g_err), "%s: all %d client slots are taken", name, h->max_clients);
+        munmap(m, (size_t)sb.st_size);
+        close(fd);
+        return QCC_EFULL;
+    }
+    qcc* c = (qcc*)calloc(1, sizeof(qcc));
+    c->fd = fd;
+    c->bytes = (size_t)sb.st_size;
+    c->shm = m;
+    c->hdr = h;
+    c->slot = &slots[idx];
+    c->index = idx;
+    c->psi = (double*)(m + h->psi_off) + (size_t)idx * 2 * (size_t)h->N;
+    c->obs = (double*)(m + h->obs_off) + (size_t)idx * QCS_MAX_OBS;
+    c->slot->pid = (int32_t)getpid();
+    __atomic_add_fetch(&h->n_clients, 1u, __ATOMIC_SEQ_CST);
+    /* the env starts on seed 0's stream, whatever an earlier owner of the slot left (the plain drop-in's state
+     * before the first set_seed) */
+    const int rc = qcc_set_seed(c, 0u);
+    if (rc) {
+        snprintf(g_err, sizeof(g_err), "%s", c->err);
+        qcc_close(c);
+        return rc;
+    }
+    *out = c;
+    return QCC_OK;
+}
+
+void qcc_close(qcc* c) {
+    if (!c) return;
+    /* a request still pending is completed first (its slot must not be re-claimed mid-tick) */
+    while (__atomic_load_n(&c->slot->done, __ATOMIC_ACQUIRE) != __atomic_load_n(&c->slot->req, __ATOMIC_RELAXED) &&
+           __atomic_load_n(&c->hdr->alive, __ATOMIC_ACQUIRE))
+        usleep(100);
+    c->slot->pid = 0;
+    __atomic_sub_fetch(&c->hdr->n_clients, 1u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&c->slot->owner, 0u, __ATOMIC_RELEASE);
+    munmap(c->shm, c->bytes);
+    close(c->fd);
+    free(c);
+}
+
+const char* qcc_last_error(const qcc* c) { return c ? c->err : g_err; }
+int qcc_dim(const qcc* c) { return c ? c->hdr->N : QCC_EINVAL; }
+int qcc_n_obs(const qcc* c) { return c ? c->hdr->n_obs : QCC_EINVAL; }
+int qcc_family(const qcc* c) { return c ? c->hdr->family : QCC_EINVAL; }
+int qcc_slot(const qcc* c) { return c ? c->index : QCC_EINVAL; }
+
+int qcc_settings(const qcc* c, double* out) {
+    if (!c || !out) return QCC_EINVAL;
+    const qcs_header* h = c->hdr;
+    out[0] = h->n_max;
+    out[1] = h->omega;
+    out[2] = h->x_max;
+    out[3] = h->grid_size;
+    out[4] = h->lambda_;
+    out[5] = h->mass;
+    out[6] = h->moment_order;
+    out[7] = h->f_max;
+    out[8] = h->n_actions;
+    return QCC_OK;
+}
+
+/* post the slot's filled request and wait for its results */
+static int call(qcc* c) {
+    qcs_slot* s = c->slot;
+    qcs_header* h = c->hdr;
+    const uint32_t r = __atomic_load_n(&s->req, __ATOMIC_RELAXED) + 1u;
+    __atomic_store_n(&s->req, r, __ATOMIC_SEQ_CST);
+    if (__atomic_load_n(&h->server_sleeping, __ATOMIC_SEQ_CST)) {
+        __atomic_add_fetch(&h->kick, 1u, __ATOMIC_SEQ_CST);
+        syscall(SYS_futex, &h->kick, FUTEX_WAKE, 1, NULL, NULL, 0);
+    }
+    /* a short spin (a tick takes tens of microseconds), then sleep on the tick word */
+    for (int i = 0; i < 2000; ++i) {
+        if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) return s->status;
+        __builtin_ia32_pause();
+    }
+    const double t0 = now_s();
+    for (;;) {
+        __atomic_store_n(&s->waiting, 1u, __ATOMIC_SEQ_CST);
+        const uint32_t t = __atomic_load_n(&h->tick, __ATOMIC_SEQ_CST);
+        if (__atomic_load_n(&s->done, __ATOMIC_SEQ_CST) == r) break;
+        struct timespec ts = {0, 20000000L};   /* 20 ms: re-check the server's liveness */
+        syscall(SYS_futex, &h->tick, FUTEX_WAIT, t, &ts, NULL, 0);
+        if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) break;
+        if (!__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) {
+            __atomic_store_n(&s->waiting, 0u, __ATOMIC_RELAXED);
+            set_err(c, "the step server stopped");
+            return QCC_ENOSERVER;
+        }
+        if (now_s() - t0 > 600.0) {
+            __atomic_store_n(&s->waiting, 0u, __ATOMIC_RELAXED);
+            set_err(c, "no answer from the step server in 600 s");
+            return QCC_ENOSERVER;
+        }
+    }
+    __atomic_store_n(&s->waiting, 0u, __ATOMIC_RELAXED);
+    if (s->status) set_err(c, s->err);
+    return s->status;
+}
+
+int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gamma, double* q, double* xmean,
+             int32_t* fail) {
+    if (!c || !psi || (n != 1 && n != 10)) return QCC_EINVAL;
+    const size_t bytes = sizeof(double) * 2 * (size_t)c->hdr->N;
+    memcpy(c->psi, psi, bytes);
+    qcs_slot* s = c->slot;
+    s->op = QCS_OP_STEP;
+    s->n = n;
+    s->dt = dt;
+    s->force = force;
+    s->gamma = gamma;
+    const int rc = call(c);
+    if (rc) return rc;
+    memcpy(psi, c->psi, bytes);
+    if (q) *q = s->q;
+    if (xmean) *xmean = s->xmean;
+    if (fail) *fail = s->fail;
+    return QCC_OK;
+}
+
+int qcc_set_seed(qcc* c, uint32_t seed) {
+    if (!c) return QCC_EINVAL;
+    c->slot->op = QCS_OP_SET_SEED;
+    c->slot->seed = seed;
+    return call(c);
+}
+
+int qcc_x_expectation(qcc* c, const double* psi, double* out) {
+    if (!c || !psi || !out) return QCC_EINVAL;
+    memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
+    c->slot->op = QCS_OP_X_EXPECT;
+    const int rc = call(c);
+    if (rc == QCC_OK) *out = c->slot->value;
+    return rc;
+}
+
+int qcc_moments(qcc* c, const double* psi, double* out) {
+    if (!c || !psi || !out) return QCC_EINVAL;
+    memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
+    c->slot->op = c->hdr->family >= 2 ? QCS_OP_MOMENTS : QCS_OP_FOCK_OBS;
+    const int rc = call(c);
+    if (rc == QCC_OK) memcpy(out, c->obs, sizeof(double) * (size_t)c->hdr->n_obs);
+    return rc;
+}

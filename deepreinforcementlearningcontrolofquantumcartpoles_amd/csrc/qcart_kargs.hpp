@@ -152,7 +152,7 @@ int launch_wavefunction(const void* psi, int precision, int64_t B, int32_t N, in
 // reference noise stream (qcart_noise.hip): per-env MT19937 state [B][kMtWords] uint32 (624 words,
 // the read index, one pad word)
 constexpr int kMtWords = 626;
-int launch_mt_seed(const uint32_t* seeds, int64_t B, uint32_t* st, void* stream);
+int launch_mt_seed(const uint32_t* seeds, const uint8_t* mask, int64_t B, uint32_t* st, void* stream);
 int launch_mt_normals(uint32_t* st, int64_t B, int32_t n_steps, const int32_t* env_steps, double* noise,
                       void* stream);
 int launch_fill_u64(uint64_t* p, int64_t n, uint64_t v, void* stream);

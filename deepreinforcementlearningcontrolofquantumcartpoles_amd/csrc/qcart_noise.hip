@@ -41,11 +41,13 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 }
 
 // init_by_array({seed}, 1) of mt19937ar.c (the serial part runs on lane 0 over the wave's LDS copy)
-__global__ __launch_bounds__(256) void k_mt_seed(const uint32_t* seeds, int64_t B, uint32_t* st) {
+// mask (optional, [B]): only envs with mask[e] != 0 are (re)seeded, the others keep their streams
+__global__ __launch_bounds__(256) void k_mt_seed(const uint32_t* seeds, const uint8_t* mask, int64_t B, uint32_t* st) {
     __shared__ uint32_t lds[4][kN];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e = (int64_t)blockIdx.x * 4 + w;
     if (e >= B) return;
+    if (mask && !mask[e]) return;
     uint32_t* mt = lds[w];
     if (lane == 0) {
         const uint32_t key = seeds[e];
@@ -144,9 +146,9 @@ __global__ __launch_bounds__(256) void k_fill_u64(uint64_t* p, int64_t n, uint64
 
 }  // namespace
 
-int launch_mt_seed(const uint32_t* seeds, int64_t B, uint32_t* st, void* stream) {
+int launch_mt_seed(const uint32_t* seeds, const uint8_t* mask, int64_t B, uint32_t* st, void* stream) {
     if (B <= 0) return 0;
-    hipLaunchKernelGGL(k_mt_seed, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, seeds, B, st);
+    hipLaunchKernelGGL(k_mt_seed, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, seeds, mask, B, st);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

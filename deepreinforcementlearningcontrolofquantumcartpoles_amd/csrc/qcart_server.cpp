@@ -1,0 +1,407 @@
+// qcart_server.cpp — the step server: the reference's process model (P actor processes, each with its own
+// `simulation` module stepping ONE env per call, IHO/main_parallel.py:345-359, :264) served by one process that
+// owns the GPU. Clients (qcart_client.c, libqcart_client.so, no HIP) post their state into a shared-memory slot
+// (qcart_shm.h); every tick the server steps all pending envs in ONE batched launch of its handle (env e = slot
+// e): the per-process H2D copy + two launches + D2H copy + sync of the plain drop-in, serialised over P HIP
+// contexts, becomes one set of launches per tick for all of them.
+//
+// A tick: wait until every owned slot has a pending request or batch_wait_us has passed since the first one;
+// copy the pending states into the server's pinned, device-mapped work rows (the kernels read and write them
+// in place: no hipMemcpy); per-env MT19937 reseeds (masked), the step envs grouped by physics-step count and
+// (dt, gamma) — each group one qc_step with a per-env step budget (env_steps: the others stay frozen) — then
+// x_expectation / moments over the batch; one stream synchronisation; results back into the slots; done = req.
+#include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/qcart.h"
+#include "qcart_shm.h"
+
+namespace {
+
+int futex_wait(uint32_t* addr, uint32_t val, long timeout_ns) {
+    struct timespec ts = {timeout_ns / 1000000000L, timeout_ns % 1000000000L};
+    return (int)syscall(SYS_futex, addr, FUTEX_WAIT, val, &ts, nullptr, 0);
+}
+void futex_wake(uint32_t* addr, int n) { syscall(SYS_futex, addr, FUTEX_WAKE, n, nullptr, nullptr, 0); }
+
+inline uint32_t ld_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+template <typename T>
+int host_alloc(T** h, T** d, size_t n) {
+    if (hipHostMalloc((void**)h, n * sizeof(T), hipHostMallocMapped) != hipSuccess) return QC_ENOMEM;
+    std::memset(*h, 0, n * sizeof(T));
+    if (hipHostGetDevicePointer((void**)d, *h, 0) != hipSuccess) return QC_EHIP;
+    return QC_OK;
+}
+
+}  // namespace
+
+struct qc_server {
+    qc_params p{};
+    int device = 0;
+    int P = 0, N = 0, n_obs = 0;
+    double wait_us = 40.0;
+    std::string name, err;
+    qc_handle* h = nullptr;
+    hipStream_t stream = nullptr;
+    // shared memory
+    int fd = -1;
+    size_t shm_bytes = 0;
+    uint8_t* shm = nullptr;
+    qcs_header* hdr = nullptr;
+    qcs_slot* slots = nullptr;
+    double* spsi = nullptr;   // [P][2N] the clients' rows
+    double* sobs = nullptr;   // [P][QCS_MAX_OBS]
+    // pinned, device-mapped work buffers (host pointer, device pointer)
+    double *psi = nullptr, *d_psi = nullptr;         // [P][2N]
+    int32_t *act = nullptr, *d_act = nullptr;        // [P]
+    int32_t *st1 = nullptr, *d_st1 = nullptr;        // [P] step budgets of the 1-step group
+    int32_t *st10 = nullptr, *d_st10 = nullptr;      // [P] ... of the 10-step group
+    uint32_t *seeds = nullptr, *d_seeds = nullptr;   // [P]
+    uint8_t *mask = nullptr, *d_mask = nullptr;      // [P]
+    double *q1 = nullptr, *d_q1 = nullptr, *xm1 = nullptr, *d_xm1 = nullptr;     // [1][P]
+    double *q10 = nullptr, *d_q10 = nullptr, *xm10 = nullptr, *d_xm10 = nullptr; // [10][P]
+    int32_t *fs1 = nullptr, *d_fs1 = nullptr, *fb10 = nullptr, *d_fb10 = nullptr; // [P]
+    double *xe = nullptr, *d_xe = nullptr;           // [P]
+    double *obs = nullptr, *d_obs = nullptr;         // [P][n_obs]
+    std::vector<uint32_t> served;                    // last served req per slot
+    std::map<double, int> custom;                    // off-grid force -> slot
+    double cur_dt = 0, cur_gamma = 0;
+    std::atomic<int> stop{0};
+    int64_t ticks = 0, calls = 0;
+};
+
+namespace {
+
+int sfail(qc_server* s, int code, const std::string& msg) {
+    if (s) s->err = msg;
+    return code;
+}
+
+// force -> action slot, as the drop-in (simulation.py _slot): the 21-level grid, else a cached custom slot
+int slot_of(qc_server* s, double force, int& slot) {
+    const int half = s->p.n_actions / 2;
+    const double spacing = s->p.f_max / half;
+    const double a = std::nearbyint(force / spacing);
+    if (a >= -half && a <= half && a * spacing == force) {
+        slot = (int)a + half;
+        return QC_OK;
+    }
+    auto it = s->custom.find(force);
+    if (it != s->custom.end()) {
+        slot = it->second;
+        return QC_OK;
+    }
+    const int rc = qc_add_force(s->h, force);
+    if (rc < 0) return rc;
+    s->custom[force] = rc;
+    slot = rc;
+    return QC_OK;
+}
+
+void free_server(qc_server* s) {
+    if (s->h) qc_destroy(s->h);
+    void* hb[] = {s->psi, s->act, s->st1, s->st10, s->seeds, s->mask, s->q1, s->xm1, s->q10, s->xm10, s->fs1, s->fb10,
+                  s->xe, s->obs};
+    for (void* b : hb)
+        if (b) (void)hipHostFree(b);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->shm) {
+        if (s->hdr) __atomic_store_n(&s->hdr->alive, 0u, __ATOMIC_SEQ_CST);
+        munmap(s->shm, s->shm_bytes);
+    }
+    if (s->fd >= 0) close(s->fd);
+    if (!s->name.empty()) shm_unlink(s->name.c_str());
+}
+
+// one tick over the pending slots `pend`
+void serve_tick(qc_server* s, const std::vector<int>& pend) {
+    const int P = s->P, N = s->N;
+    struct Req { int op, n; uint32_t seed; double dt, force, gamma; };
+    std::vector<Req> rq(P);
+    bool any_seed = false, any_x = false, any_obs = false;
+    std::vector<int> g1, g10;   // step groups
+    for (int e : pend) {
+        qcs_slot& sl = s->slots[e];
+        Req r{sl.op, sl.n, sl.seed, sl.dt, sl.force, sl.gamma};
+        rq[e] = r;
+        sl.status = QC_OK;
+        sl.err[0] = 0;
+        if (r.op == QCS_OP_SET_SEED) {
+            s->seeds[e] = r.seed;
+            s->mask[e] = 1;
+            any_seed = true;
+            continue;
+        }
+        std::memcpy(s->psi + (size_t)e * 2 * N, s->spsi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
+        if (r.op == QCS_OP_STEP) (r.n == 10 ? g10 : g1).push_back(e);
+        else if (r.op == QCS_OP_X_EXPECT) any_x = true;
+        else any_obs = true;
+    }
+    auto err_all = [&](const std::vector<int>& es, int rc) {
+        const char* m = qc_last_error(s->h);
+        for (int e : es) {
+            s->slots[e].status = rc;
+            std::snprintf(s->slots[e].err, sizeof(s->slots[e].err), "%s", m ? m : "");
+        }
+    };
+    if (any_seed) {
+        std::vector<int> es;
+        for (int e : pend) if (rq[e].op == QCS_OP_SET_SEED) es.push_back(e);
+        const int rc = qc_set_seed_mt19937_envs(s->h, s->d_seeds, s->d_mask);
+        if (rc) err_all(es, rc);
+    }
+    // step groups: by step count, then by (dt, gamma) (one set of tables per handle: the drivers pass the same
+    // dt and gamma on every call; a change rebuilds them, as the reference's reset_ab on a dt change)
+    for (int grp = 0; grp < 2; ++grp) {
+        const std::vector<int>& G = grp == 0 ? g1 : g10;
+        std::vector<int> rest = G;
+        while (!rest.empty()) {
+            const double dt = rq[rest[0]].dt, gamma = rq[rest[0]].gamma;
+            std::vector<int> now, later;
+            for (int e : rest) ((rq[e].dt == dt && rq[e].gamma == gamma) ? now : later).push_back(e);
+            rest = later;
+            int rc = QC_OK;
+            if (dt != s->cur_dt || gamma != s->cur_gamma) {
+                (void)hipStreamSynchronize(s->stream);
+                rc = qc_set_dynamics(s->h, dt, gamma);
+                if (rc == QC_OK) { s->cur_dt = dt; s->cur_gamma = gamma; }
+            }
+            int32_t* stb = grp == 0 ? s->st1 : s->st10;
+            if (!later.empty()) (void)hipStreamSynchronize(s->stream);   // the budget array is read by the kernels
+            std::memset(stb, 0, sizeof(int32_t) * P);
+            std::vector<int> ok;
+            for (int e : now) {
+                int sl = 0;
+                const int r2 = rc ? rc : slot_of(s, rq[e].force, sl);
+                if (r2) { err_all({e}, r2); continue; }
+                s->act[e] = sl;
+                stb[e] = grp == 0 ? 1 : 10;
+                ok.push_back(e);
+            }
+            if (ok.empty()) continue;
+            const int n = grp == 0 ? 1 : 10;
+            rc = qc_step(s->h, s->d_psi, s->d_act, s->p.n_actions / 2, n, grp == 0 ? s->d_st1 : s->d_st10, nullptr,
+                         grp == 0 ? s->d_q1 : s->d_q10, grp == 0 ? s->d_xm1 : s->d_xm10, grp == 0 ? s->d_fs1 : nullptr,
+                         nullptr, nullptr);
+            // simulate_10_steps' Fail is the boundary test of the final state (IHO/simulation_i.cpp:391-421)
+            if (rc == QC_OK && grp == 1) rc = qc_boundary_fail(s->h, s->d_psi, s->d_fb10);
+            if (rc) err_all(ok, rc);
+        }
+    }
+    if (any_x) {
+        const int rc = qc_x_expectation(s->h, s->d_psi, s->d_xe);
+        if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op == QCS_OP_X_EXPECT) es.push_back(e); err_all(es, rc); }
+    }
+    if (any_obs) {
+        const int rc = qc_moments(s->h, s->d_psi, s->d_obs);
+        if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op >= QCS_OP_MOMENTS) es.push_back(e); err_all(es, rc); }
+    }
+    if (hipStreamSynchronize(s->stream) != hipSuccess) {
+        qc_sync(s->h);
+        err_all(pend, QC_EHIP);
+    }
+    if (qc_take_errors(s->h) != 0) err_all(pend, QC_EINVAL);
+    for (int e : pend) {
+        qcs_slot& sl = s->slots[e];
+        const Req& r = rq[e];
+        if (sl.status == QC_OK) {
+            if (r.op == QCS_OP_STEP) {
+                std::memcpy(s->spsi + (size_t)e * 2 * N, s->psi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
+                if (r.n == 10) {
+                    sl.q = s->q10[(size_t)9 * P + e];
+                    sl.xmean = s->xm10[(size_t)9 * P + e];
+                    sl.fail = s->fb10[e] ? 1 : 0;
+                } else {
+                    sl.q = s->q1[e];
+                    sl.xmean = s->xm1[e];
+                    sl.fail = s->fs1[e] > 0 ? 1 : 0;
+                }
+            } else if (r.op == QCS_OP_X_EXPECT) {
+                sl.value = s->xe[e];
+            } else if (r.op == QCS_OP_MOMENTS || r.op == QCS_OP_FOCK_OBS) {
+                std::memcpy(s->sobs + (size_t)e * QCS_MAX_OBS, s->obs + (size_t)e * s->n_obs, sizeof(double) * s->n_obs);
+            }
+        }
+        s->mask[e] = 0;
+        s->served[e] = __atomic_load_n(&sl.req, __ATOMIC_RELAXED);
+        __atomic_store_n(&sl.done, s->served[e], __ATOMIC_SEQ_CST);
+    }
+    s->ticks++;
+    s->calls += (int64_t)pend.size();
+    s->hdr->ticks = (uint64_t)s->ticks;
+    s->hdr->calls = (uint64_t)s->calls;
+    __atomic_add_fetch(&s->hdr->tick, 1u, __ATOMIC_SEQ_CST);
+    bool wake = false;
+    for (int e : pend) wake = wake || __atomic_load_n(&s->slots[e].waiting, __ATOMIC_SEQ_CST);
+    if (wake) futex_wake(&s->hdr->tick, 1 << 30);
+}
+
+void scan(qc_server* s, std::vector<int>& pend, int& owned) {
+    pend.clear();
+    owned = 0;
+    for (int e = 0; e < s->P; ++e) {
+        if (!ld_acq(&s->slots[e].owner)) continue;
+        ++owned;
+        if (ld_acq(&s->slots[e].req) != s->served[e]) pend.push_back(e);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int qc_server_create(const qc_params* p, int device, int32_t max_clients, const char* name, double batch_wait_us,
+                     qc_server** out) {
+    if (!out || !p || !name || !*name || name[0] != '/' || max_clients < 1 || max_clients > 4096) return QC_EINVAL;
+    *out = nullptr;
+    if (p->precision != QC_FP64) return QC_EINVAL;   // the drop-in computes in fp64 like the reference
+    qc_server* s = new qc_server();
+    s->p = *p;
+    s->p.batch = max_clients;
+    s->p.env_offset = 0;
+    s->device = device;
+    s->P = max_clients;
+    s->wait_us = batch_wait_us > 0 ? batch_wait_us : 40.0;
+    int rc = qc_create(&s->p, device, &s->h);
+    if (rc) { delete s; return rc; }
+    s->N = qc_dim(s->h);
+    s->n_obs = qc_n_obs(s->h);
+    s->cur_dt = p->dt;
+    s->cur_gamma = p->gamma;
+    const int P = s->P, N = s->N;
+    auto bail = [&](int code, const std::string& m) { s->err = m; free_server(s); delete s; return code; };
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(QC_EHIP, "hipStreamCreate failed");
+    qc_set_stream(s->h, s->stream);
+    if (host_alloc(&s->psi, &s->d_psi, (size_t)P * 2 * N) || host_alloc(&s->act, &s->d_act, P) ||
+        host_alloc(&s->st1, &s->d_st1, P) || host_alloc(&s->st10, &s->d_st10, P) || host_alloc(&s->seeds, &s->d_seeds, P) ||
+        host_alloc(&s->mask, &s->d_mask, P) || host_alloc(&s->q1, &s->d_q1, P) || host_alloc(&s->xm1, &s->d_xm1, P) ||
+        host_alloc(&s->q10, &s->d_q10, (size_t)10 * P) || host_alloc(&s->xm10, &s->d_xm10, (size_t)10 * P) ||
+        host_alloc(&s->fs1, &s->d_fs1, P) || host_alloc(&s->fb10, &s->d_fb10, P) || host_alloc(&s->xe, &s->d_xe, P) ||
+        host_alloc(&s->obs, &s->d_obs, (size_t)P * (s->n_obs > 0 ? s->n_obs : 1)))
+        return bail(QC_ENOMEM, "pinned host buffers");
+    // every env starts on seed 0's MT19937 stream (the plain drop-in's state before the first set_seed)
+    rc = qc_set_seed_mt19937(s->h, s->d_seeds);
+    if (rc == QC_OK) rc = qc_sync(s->h);
+    if (rc) return bail(rc, "initial MT19937 seeding failed");
+    // the shared-memory object
+    const size_t slot_off = round_up(sizeof(qcs_header), 4096);
+    const size_t psi_off = round_up(slot_off + sizeof(qcs_slot) * P, 4096);
+    const size_t obs_off = round_up(psi_off + sizeof(double) * 2 * N * P, 4096);
+    const size_t total = round_up(obs_off + sizeof(double) * QCS_MAX_OBS * P, 4096);
+    s->fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (s->fd < 0) return bail(QC_EINVAL, std::string("shm_open(") + name + "): " + strerror(errno));
+    s->name = name;
+    if (ftruncate(s->fd, (off_t)total) != 0) return bail(QC_ENOMEM, "ftruncate");
+    void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, s->fd, 0);
+    if (m == MAP_FAILED) return bail(QC_ENOMEM, "mmap");
+    s->shm = (uint8_t*)m;
+    s->shm_bytes = total;
+    std::memset(s->shm, 0, total);
+    s->hdr = (qcs_header*)s->shm;
+    s->slots = (qcs_slot*)(s->shm + slot_off);
+    s->spsi = (double*)(s->shm + psi_off);
+    s->sobs = (double*)(s->shm + obs_off);
+    qcs_header* H = s->hdr;
+    H->magic = QCS_MAGIC;
+    H->version = QCS_VERSION;
+    H->max_clients = P;
+    H->N = N;
+    H->n_obs = s->n_obs;
+    H->family = p->family;
+    H->slot_off = slot_off;
+    H->psi_off = psi_off;
+    H->obs_off = obs_off;
+    H->total_bytes = total;
+    H->n_max = p->n_max;
+    H->moment_order = p->moment_order;
+    H->omega = p->omega;
+    H->x_max = p->x_max;
+    H->grid_size = p->grid_size;
+    H->lambda_ = p->lambda_;
+    H->mass = p->mass;
+    H->f_max = p->f_max;
+    H->n_actions = p->n_actions;
+    s->served.assign(P, 0u);
+    __atomic_store_n(&H->alive, 1u, __ATOMIC_SEQ_CST);
+    *out = s;
+    return QC_OK;
+}
+
+int qc_server_run(qc_server* s, double seconds) {
+    if (!s) return QC_EINVAL;
+    if (hipSetDevice(s->device) != hipSuccess) return sfail(s, QC_EHIP, "hipSetDevice");
+    const double t_end = seconds > 0 ? now_us() + seconds * 1e6 : 1e300;
+    std::vector<int> pend;
+    int owned = 0;
+    double idle_since = now_us();
+    while (!s->stop.load(std::memory_order_relaxed) && now_us() < t_end) {
+        scan(s, pend, owned);
+        if (pend.empty()) {
+            if (now_us() - idle_since < 200.0) {   // short spin: the next request is usually microseconds away
+                for (int i = 0; i < 64; ++i) cpu_relax();
+                continue;
+            }
+            // asleep until a client kicks (or 2 ms): a client posting while server_sleeping is set wakes us
+            const uint32_t k = __atomic_load_n(&s->hdr->kick, __ATOMIC_SEQ_CST);
+            __atomic_store_n(&s->hdr->server_sleeping, 1u, __ATOMIC_SEQ_CST);
+            scan(s, pend, owned);
+            if (pend.empty()) futex_wait(&s->hdr->kick, k, 2000000L);
+            __atomic_store_n(&s->hdr->server_sleeping, 0u, __ATOMIC_SEQ_CST);
+            continue;
+        }
+        // batch: wait (briefly) for the other owned slots' requests of this tick
+        const double t0 = now_us();
+        while ((int)pend.size() < owned && now_us() - t0 < s->wait_us) {
+            for (int i = 0; i < 32; ++i) cpu_relax();
+            scan(s, pend, owned);
+        }
+        serve_tick(s, pend);
+        idle_since = now_us();
+    }
+    return QC_OK;
+}
+
+int qc_server_stop(qc_server* s) {
+    if (!s) return QC_EINVAL;
+    s->stop.store(1);
+    if (s->hdr) futex_wake(&s->hdr->kick, 1);
+    return QC_OK;
+}
+
+int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls) {
+    if (!s) return QC_EINVAL;
+    if (ticks) *ticks = s->ticks;
+    if (calls) *calls = s->calls;
+    return QC_OK;
+}
+
+const char* qc_server_last_error(const qc_server* s) { return s ? s->err.c_str() : ""; }
+
+void qc_server_destroy(qc_server* s) {
+    if (!s) return;
+    free_server(s);
+    delete s;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+/*
+ * qcart_shm.h — the shared-memory protocol between the step server (qcart_server.cpp, inside libqcart.so, the
+ * one process that owns the GPU) and its actor-process clients (qcart_client.c, libqcart_client.so: plain C, no
+ * HIP). It reproduces the reference's process model — 30-40 actor processes, each calling its own `simulation`
+ * module on one env (IHO/main_parallel.py:345-359, :264) — with every pending env of a tick stepped in ONE
+ * batched launch on the server's handle (env e = client slot e).
+ *
+ * One POSIX shared-memory object /dev/shm/<name>:
+ *   [qcs_header][qcs_slot x max_clients][psi: max_clients x N complex128][obs: max_clients x kQcsMaxObs fp64]
+ * A client owns its slot's request fields, its psi row and obs row between calls; the server reads them only
+ * while the slot has a pending request (req != done) and writes the results before publishing done = req.
+ * Synchronisation: GCC __atomic builtins (C and C++ alike) on 32-bit words; sleeping sides wait on futexes of
+ * the shared mapping (clients on header.tick, the server on header.kick).
+ */
+#ifndef QCART_SHM_H
+#define QCART_SHM_H
+
+#include <stdint.h>
+
+#define QCS_MAGIC 0x56534351u /* "QCSV" */
+#define QCS_VERSION 1u
+#define QCS_MAX_OBS 64        /* >= the largest n_obs ((2+9+1)*9/2 = 54 grid moments) */
+
+/* request operations (the reference module's functions, IHO/simulation_i.cpp:618-631, QO/simulation_quart.cpp:656-668) */
+enum qcs_op {
+    QCS_OP_STEP = 1,       /* step(state, dt, force, gamma): n = 1; simulate_10_steps: n = 10 (Fail of the final state) */
+    QCS_OP_SET_SEED = 2,   /* set_seed(seed): the env's MT19937 stream restarts */
+    QCS_OP_X_EXPECT = 3,   /* x_expectation(state) */
+    QCS_OP_MOMENTS = 4,    /* get_moments(state, data) (grid) */
+    QCS_OP_FOCK_OBS = 5    /* the Fock 'xp' 5-vector (IHO/main_parallel.py:129-131) */
+};
+
+typedef struct qcs_header {
+    uint32_t magic, version;
+    int32_t max_clients, N, n_obs, family;
+    uint32_t alive;          /* 1 while the server serves; 0 after it stopped (clients fail their calls) */
+    uint32_t tick;           /* incremented (and futex-woken) after every served tick */
+    uint32_t kick;           /* incremented (and futex-woken) by a client whose request finds the server asleep */
+    uint32_t server_sleeping;
+    uint32_t n_clients;      /* slots currently owned */
+    uint32_t pad0;
+    uint64_t slot_off, psi_off, obs_off, total_bytes;
+    /* the module's compiled parameters (check_settings) */
+    int32_t n_max, moment_order;
+    double omega, x_max, grid_size, lambda_, mass, f_max;
+    int32_t n_actions, pad1;
+    uint64_t ticks, calls;   /* served ticks / requests (statistics, server-written) */
+} qcs_header;
+
+typedef struct qcs_slot {
+    uint32_t owner;          /* 0 free, 1 owned (claimed by CAS in qcc_open) */
+    int32_t pid;
+    uint32_t req;            /* the client's request sequence number (incremented to post a request) */
+    uint32_t done;           /* = req once the server has written the results */
+    uint32_t waiting;        /* the client sleeps on header.tick */
+    int32_t op, n;
+    uint32_t seed;
+    double dt, force, gamma;
+    int32_t status;          /* 0 ok, < 0 a qc_status code */
+    int32_t fail;            /* step: Fail */
+    double q, xmean;         /* step: the last step's q and x_mean */
+    double value;            /* x_expectation */
+    char err[96];
+    uint8_t pad[32];
+} qcs_slot;
+
+#endif

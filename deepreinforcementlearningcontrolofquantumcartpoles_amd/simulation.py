@@ -18,6 +18,13 @@ seed), two Box-Muller normals per step (qc_set_seed_mt19937; MKL's uniform words
 normals to <= 1 ulp of MKL's CBWR=COMPATIBLE path, tests/test_mkl_fixtures.py). Before the first
 set_seed the module, like the reference's, has no seeded stream; here it draws from seed 0's.
 load(..., noise="philox") selects the counter-based Philox stream instead.
+
+The reference's process model — 30-40 actor processes, each with its own module stepping one env
+(IHO/main_parallel.py:345-359) — runs through a step server: one process owns the GPU (StepServer / serve(),
+qc_server_* in libqcart) and each actor calls load(..., server="/name") (or install(...)), whose functions post
+requests through shared memory (libqcart_client.so, plain C: the actor process never creates a HIP context) and
+are served for every pending actor in one batched launch per tick. Same names, arguments, return values, errors
+and per-env MT19937 stream as the module above.
 """
 from __future__ import annotations
 
@@ -166,19 +173,210 @@ class _Simulation:
         return None
 
 
-def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", **params) -> types.ModuleType:
+# ---------------------------------------------------------------------------- step server (many actor processes)
+_CLIENT_LIB = None
+
+
+def _client_lib():
+    """libqcart_client.so (include/qcart_client.h): plain C, no HIP — loading it never touches the GPU."""
+    global _CLIENT_LIB
+    if _CLIENT_LIB is None:
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqcart_client.so")
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built: run `make`")
+        L = ctypes.CDLL(path)
+        vp, d, i32, P = ctypes.c_void_p, ctypes.c_double, ctypes.c_int32, ctypes.POINTER
+        L.qcc_open.argtypes = [ctypes.c_char_p, P(vp)]
+        L.qcc_close.argtypes = [vp]
+        L.qcc_close.restype = None
+        L.qcc_last_error.argtypes = [vp]
+        L.qcc_last_error.restype = ctypes.c_char_p
+        for f in ("qcc_dim", "qcc_n_obs", "qcc_family", "qcc_slot"):
+            getattr(L, f).argtypes = [vp]
+        L.qcc_settings.argtypes = [vp, vp]
+        L.qcc_step.argtypes = [vp, vp, i32, d, d, d, P(d), P(d), P(i32)]
+        L.qcc_set_seed.argtypes = [vp, ctypes.c_uint32]
+        L.qcc_x_expectation.argtypes = [vp, vp, P(d)]
+        L.qcc_moments.argtypes = [vp, vp, vp]
+        _CLIENT_LIB = L
+    return _CLIENT_LIB
+
+
+class _ServedSimulation:
+    """One actor's `simulation` module served by a StepServer (one slot = one env of the server's batch)."""
+
+    def __init__(self, physics: cfg.Physics, server: str):
+        L = _client_lib()
+        c = ctypes.c_void_p()
+        rc = L.qcc_open(server.encode(), ctypes.byref(c))
+        if rc != 0:
+            raise RuntimeError("Initialization Failure: " + (L.qcc_last_error(None) or b"").decode())
+        self._L, self._c = L, c
+        self.physics = physics
+        self.N = L.qcc_dim(c)
+        self.n_obs = L.qcc_n_obs(c)
+        st = np.zeros(9)
+        L.qcc_settings(c, st.ctypes.data)
+        fam = L.qcc_family(c)
+        # the drivers' compile check (check_C_module_and_compile, IHO/main_parallel.py:564-583): the server's
+        # module must carry this actor's parameters
+        want = (physics.n_max, physics.omega) if physics.fock else (physics.x_max, physics.grid_size, physics.lambda_,
+                                                                     physics.mass, physics.moment_order)
+        have = (int(st[0]), st[1]) if physics.fock else (st[2], st[3], st[4], st[5], int(st[6]))
+        if fam != physics.family or want != have:
+            self.close()
+            raise RuntimeError(f"step server {server} serves family {fam} {have}, not {physics.family} {want}")
+        self._q, self._xm, self._f = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+        self._v = ctypes.c_double()
+
+    def close(self):
+        if getattr(self, "_c", None):
+            self._L.qcc_close(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            msg = (self._L.qcc_last_error(self._c) or b"").decode()
+            raise RuntimeError(f"step server: {msg} ({rc})")
+
+    def set_seed(self, seed):
+        if not isinstance(seed, (int, np.integer)):
+            raise TypeError("seed must be an int")
+        self._check(self._L.qcc_set_seed(self._c, int(seed) & 0xFFFFFFFF))
+
+    def check_settings(self):
+        p = self.physics
+        return (p.n_max, p.omega) if p.fock else (self.N, p.grid_size, p.lambda_, p.mass, p.moment_order)
+
+    def _run(self, state, dt, force, gamma, n):
+        _check_state(state, self.N)
+        if not state.flags.c_contiguous or not state.flags.writeable:
+            raise ValueError("The input array is not a writeable contiguous array")
+        self._check(self._L.qcc_step(self._c, state.ctypes.data, n, float(dt), float(force), float(gamma),
+                                     ctypes.byref(self._q), ctypes.byref(self._xm), ctypes.byref(self._f)))
+        return self._q.value, self._xm.value, int(self._f.value)
+
+    def step(self, state, dt, force, gamma):
+        return self._run(state, dt, force, gamma, 1)
+
+    def simulate_10_steps(self, state, dt, force, gamma):
+        return self._run(state, dt, force, gamma, 10)
+
+    def x_expectation(self, state):
+        _check_state(state, self.N)
+        st = np.ascontiguousarray(state)
+        self._check(self._L.qcc_x_expectation(self._c, st.ctypes.data, ctypes.byref(self._v)))
+        return self._v.value
+
+    def get_moments(self, state, data):
+        _check_state(state, self.N)
+        if not isinstance(data, np.ndarray) or data.ndim != 1:
+            raise ValueError("The moment data array is not one-dimensional")
+        if data.shape[0] != self.n_obs:
+            raise ValueError("The moment data array does not match the required size " + str(self.n_obs))
+        if data.dtype != np.float64:
+            raise ValueError("The moment data array does not match the required datatype: Float64")
+        out = np.empty(self.n_obs)
+        self._check(self._L.qcc_moments(self._c, np.ascontiguousarray(state).ctypes.data, out.ctypes.data))
+        data[:] = out
+
+
+class StepServer:
+    """The step server of the reference's process model (qc_server_*): owns the GPU and one handle of
+    `max_clients` envs; actor processes attach with load(..., server=name). run() serves on the calling
+    thread; start() / stop() on a background thread."""
+
+    def __init__(self, family: int | str = cfg.IHO, max_clients: int = 16, name: str | None = None, device: int = 0,
+                 batch_wait_us: float = 40.0, **params):
+        import os
+        import torch
+
+        from .core import make_params
+        if isinstance(family, str):
+            family = {v: k for k, v in cfg.FAMILY_NAMES.items()}[family]
+        self.physics = cfg.DEFAULTS[family].with_(**params)
+        self.name = name or f"/qcart_srv_{os.getpid()}"
+        torch.cuda.init()
+        self._L = _lib.lib()
+        p = make_params(self.physics, max_clients, seed=0)
+        h = ctypes.c_void_p()
+        rc = self._L.qc_server_create(ctypes.byref(p), device, int(max_clients), self.name.encode(),
+                                      float(batch_wait_us), ctypes.byref(h))
+        if rc != 0:
+            msg = (self._L.qc_last_error(None) or b"").decode()
+            raise _lib.QCartError(rc, f"step server {self.name}: {msg}")
+        self._h = h
+        self._thread = None
+
+    def run(self, seconds: float = 0.0):
+        rc = self._L.qc_server_run(self._h, float(seconds))
+        if rc != 0:
+            raise _lib.QCartError(rc, (self._L.qc_server_last_error(self._h) or b"").decode())
+
+    def start(self):
+        import threading
+        self._thread = threading.Thread(target=self.run, daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        if self._h:
+            self._L.qc_server_stop(self._h)
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def stats(self):
+        t, c = ctypes.c_int64(), ctypes.c_int64()
+        self._L.qc_server_stats(self._h, ctypes.byref(t), ctypes.byref(c))
+        return {"ticks": t.value, "calls": c.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.stop()
+            self._L.qc_server_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", server: str | None = None,
+         **params) -> types.ModuleType:
     """Return a module-like object equivalent to the reference's compiled `simulation` extension.
 
     family: 0/'harmonic', 1/'inverted_harmonic', 2/'quartic', 3/'inverted_quartic'; params are the
     setupC.py macros (n_max, omega / x_max, grid_size, lambda_, mass, moment_order) and optionally
     gamma, time_steps, f_max, a_mode (defaults: the drivers' values, config.DEFAULTS). noise: 'mt19937'
-    (the reference's stream, default) or 'philox'."""
+    (the reference's stream, default) or 'philox'. server: the name of a running StepServer — the module's
+    calls are then served by it (this process never touches the GPU; MT19937 noise)."""
     if isinstance(family, str):
         family = {v: k for k, v in cfg.FAMILY_NAMES.items()}[family]
     phys = cfg.DEFAULTS[family].with_(**params)
-    key = (device, noise, tuple(sorted(phys.asdict().items())))
+    key = (device, noise, server, tuple(sorted(phys.asdict().items())))
     if key not in _MODULES:
-        sim = _Simulation(phys, device, noise)
+        if server is not None:
+            if noise != "mt19937":
+                raise ValueError("a step server draws the reference's MT19937 stream (noise='mt19937')")
+            sim = _ServedSimulation(phys, server)
+        else:
+            sim = _Simulation(phys, device, noise)
         mod = types.ModuleType("simulation", "MI355X-native drop-in for the reference `simulation` module")
         for name in ("step", "simulate_10_steps", "set_seed", "check_settings", "x_expectation"):
             setattr(mod, name, getattr(sim, name))
@@ -189,12 +387,13 @@ def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", *
     return _MODULES[key]
 
 
-def install(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", **params) -> types.ModuleType:
+def install(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", server: str | None = None,
+            **params) -> types.ModuleType:
     """Register the drop-in as `simulation` in sys.modules, so the reference drivers'
-    `__import__('simulation')` resolves to it."""
-    mod = load(family, device, noise, **params)
+    `__import__('simulation')` resolves to it (server: see load)."""
+    mod = load(family, device, noise, server, **params)
     sys.modules["simulation"] = mod
     return mod
 
 
-__all__ = ["load", "install", "pi"]
+__all__ = ["load", "install", "StepServer", "pi"]

@@ -128,6 +128,9 @@ int qc_env_counters(qc_handle* h, uint64_t* out, const uint64_t* in);
 /* set_seed for every env in MT19937 mode: seeds device uint32 [B], env e's stream
  * vslNewStream(VSL_BRNG_MT19937, seeds[e]) */
 int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds);
+/* set_seed for the envs with mask[e] != 0 only (mask: device uint8 [B]); the others keep their streams — one
+ * actor process's set_seed under the step server (qc_server_*). Needs the handle in MT19937 mode. */
+int qc_set_seed_mt19937_envs(qc_handle* h, const uint32_t* seeds, const uint8_t* mask);
 int qc_noise_mode(const qc_handle* h);
 /* per-env MT19937 states (device uint32 [B][qc_mt19937_words()]: 624 state words, read index, pad):
  * copied to `out` and/or replaced from `in` */
@@ -412,6 +415,26 @@ int qc_replay_rebuild(qc_replay* r);
 int qc_replay_stats(qc_replay* r, qc_replay_stats_t* out);
 /* device pointers of the tree and the row storage (introspection, tests) */
 int qc_replay_buffers(const qc_replay* r, const double** tree, const float** data);
+
+/* ---- step server: the reference's process model on one GPU ------------------------------------------------
+ * The drivers run 30-40 actor processes, each with its own `simulation` module stepping ONE env per call
+ * (IHO/main_parallel.py:345-359, :264). A step server owns one handle of batch max_clients (env e = client slot
+ * e, MT19937 noise per env) and a POSIX shared-memory object `name` ("/..."); actor processes attach with
+ * libqcart_client.so (include/qcart_client.h, no HIP) and post step / simulate_10_steps / set_seed /
+ * x_expectation / get_moments requests. Each tick steps every pending env in one batched launch (per-env step
+ * budgets keep the others frozen); the tick waits up to batch_wait_us (<= 0: 40 us) after its first request for
+ * the other owned slots' requests. Results equal the plain drop-in's (the same kernels, the same per-env
+ * MT19937 stream). */
+typedef struct qc_server qc_server;
+int qc_server_create(const qc_params* p, int device, int32_t max_clients, const char* name, double batch_wait_us,
+                     qc_server** out);
+/* serve on the calling thread until qc_server_stop (another thread) or `seconds` (> 0) have passed */
+int qc_server_run(qc_server* s, double seconds);
+int qc_server_stop(qc_server* s);
+int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls);
+const char* qc_server_last_error(const qc_server* s);
+/* marks the object dead (waiting clients fail with QCC_ENOSERVER) and unlinks it */
+void qc_server_destroy(qc_server* s);
 
 #ifdef __cplusplus
 }

@@ -80,3 +80,21 @@ def test_moment_order_range_is_validated_before_the_device():
     rc = _lib.lib().qc_create(ctypes.byref(p), 0, ctypes.byref(h))
     assert rc == -1 and not h.value
     assert b"1..9" in _lib.lib().qc_last_error(None)
+
+
+CLIENT = os.path.join(ROOT, "deepreinforcementlearningcontrolofquantumcartpoles_amd", "libqcart_client.so")
+
+
+@pytest.mark.skipif(not os.path.exists(CLIENT), reason="libqcart_client.so not built")
+def test_client_library_exports_every_declared_symbol():
+    """libqcart_client.so (the step server's actor side, include/qcart_client.h): plain C, every declared
+    symbol exported, and no HIP runtime linked (an actor process never creates a GPU context)."""
+    import subprocess
+    txt = open(os.path.join(ROOT, "include", "qcart_client.h")).read()
+    syms = sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+\*?(qcc_\w+)\s*\(", txt, re.M)))
+    assert len(syms) >= 10
+    L = ctypes.CDLL(CLIENT)
+    for s in syms:
+        assert hasattr(L, s), s
+    deps = subprocess.run(["ldd", CLIENT], capture_output=True, text=True).stdout
+    assert "amdhip" not in deps and "hsa" not in deps

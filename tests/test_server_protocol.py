@@ -1,0 +1,188 @@
+"""The step server's shared-memory protocol on the CPU (no GPU): libqcart_client.so against a mock server
+thread that plays qcart_server.cpp's side of csrc/qcart_shm.h (slot claim, request / done sequence numbers,
+the tick futex), plus the layout mirror checked against the C header with gcc."""
+import ctypes
+import mmap
+import os
+import shutil
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "deepreinforcementlearningcontrolofquantumcartpoles_amd")
+CLIENT = os.path.join(PKG, "libqcart_client.so")
+SHM_H = os.path.join(PKG, "csrc", "qcart_shm.h")
+
+pytestmark = pytest.mark.skipif(not os.path.exists(CLIENT), reason="libqcart_client.so not built")
+
+u32, i32, u64, d = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_double
+
+
+class Header(ctypes.Structure):
+    _fields_ = [("magic", u32), ("version", u32), ("max_clients", i32), ("N", i32), ("n_obs", i32), ("family", i32),
+                ("alive", u32), ("tick", u32), ("kick", u32), ("server_sleeping", u32), ("n_clients", u32),
+                ("pad0", u32), ("slot_off", u64), ("psi_off", u64), ("obs_off", u64), ("total_bytes", u64),
+                ("n_max", i32), ("moment_order", i32), ("omega", d), ("x_max", d), ("grid_size", d), ("lambda_", d),
+                ("mass", d), ("f_max", d), ("n_actions", i32), ("pad1", i32), ("ticks", u64), ("calls", u64)]
+
+
+class Slot(ctypes.Structure):
+    _fields_ = [("owner", u32), ("pid", i32), ("req", u32), ("done", u32), ("waiting", u32), ("op", i32), ("n", i32),
+                ("seed", u32), ("dt", d), ("force", d), ("gamma", d), ("status", i32), ("fail", i32), ("q", d),
+                ("xmean", d), ("value", d), ("err", ctypes.c_char * 96), ("pad", ctypes.c_uint8 * 32)]
+
+
+OP_STEP, OP_SET_SEED, OP_X, OP_MOM, OP_FOCK = 1, 2, 3, 4, 5
+MAX_OBS = 64
+
+
+def test_layout_mirror_matches_the_c_header(tmp_path):
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    src = tmp_path / "lay.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{SHM_H}"', "int main(void){"]
+    for S, c in ((Header, "qcs_header"), (Slot, "qcs_slot")):
+        for f, _ in S._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({c}, {f}));')
+        lines.append(f'printf("%zu\\n", sizeof({c}));')
+    lines.append("return 0;}")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = []
+    for S in (Header, Slot):
+        want += [getattr(S, f).offset for f, _ in S._fields_] + [ctypes.sizeof(S)]
+    assert got == want
+
+
+class MockServer:
+    """qcart_server.cpp's side of the protocol in Python: STEP negates the state and reports q = 1.5 n,
+    x_mean = force, Fail = n == 10; SET_SEED stores the seed in `value`; X_EXPECT returns the sum of Re(psi);
+    MOMENTS fills the obs row with 0, 1, 2, ..."""
+
+    def __init__(self, name, P=3, N=8, n_obs=5):
+        self.name, self.P, self.N, self.n_obs = name, P, N, n_obs
+        rnd = lambda v: (v + 4095) // 4096 * 4096   # noqa: E731
+        self.slot_off = rnd(ctypes.sizeof(Header))
+        self.psi_off = rnd(self.slot_off + ctypes.sizeof(Slot) * P)
+        self.obs_off = rnd(self.psi_off + 16 * N * P)
+        self.total = rnd(self.obs_off + 8 * MAX_OBS * P)
+        path = "/dev/shm" + name
+        with open(path, "wb") as f:
+            f.truncate(self.total)
+        self.fd = os.open(path, os.O_RDWR)
+        self.mm = mmap.mmap(self.fd, self.total)
+        self.hdr = Header.from_buffer(self.mm, 0)
+        self.slots = (Slot * P).from_buffer(self.mm, self.slot_off)
+        self.psi = np.frombuffer(self.mm, np.complex128, N * P, self.psi_off).reshape(P, N)
+        self.obs = np.frombuffer(self.mm, np.float64, MAX_OBS * P, self.obs_off).reshape(P, MAX_OBS)
+        h = self.hdr
+        h.magic, h.version, h.max_clients, h.N, h.n_obs, h.family = 0x56534351, 1, P, N, n_obs, 1
+        h.slot_off, h.psi_off, h.obs_off, h.total_bytes = self.slot_off, self.psi_off, self.obs_off, self.total
+        h.n_max, h.omega = N - 1, 3.14159
+        h.alive = 1
+        self.served = [0] * P
+        self.stop = False
+        self.libc = ctypes.CDLL(None, use_errno=True)
+        self.t = threading.Thread(target=self.loop, daemon=True)
+        self.t.start()
+
+    def loop(self):
+        while not self.stop:
+            any_ = False
+            for e in range(self.P):
+                s = self.slots[e]
+                if not s.owner or s.req == self.served[e]:
+                    continue
+                any_ = True
+                if s.op == OP_STEP:
+                    self.psi[e] *= -1
+                    s.q, s.xmean, s.fail = 1.5 * s.n, s.force, int(s.n == 10)
+                elif s.op == OP_SET_SEED:
+                    s.value = float(s.seed)
+                elif s.op == OP_X:
+                    s.value = float(self.psi[e].real.sum())
+                else:
+                    self.obs[e, :self.n_obs] = np.arange(self.n_obs)
+                s.status = 0
+                self.served[e] = s.req
+                s.done = s.req
+            if any_:
+                self.hdr.tick += 1
+                addr = ctypes.addressof(self.hdr) + Header.tick.offset
+                self.libc.syscall(202, ctypes.c_void_p(addr), 1, 1 << 30, None, None, 0)   # FUTEX_WAKE
+            else:
+                time.sleep(0.0002)
+
+    def close(self):
+        self.stop = True
+        self.t.join()
+        self.hdr.alive = 0
+        del self.hdr, self.slots, self.psi, self.obs
+        self.mm.close()
+        os.close(self.fd)
+        os.unlink("/dev/shm" + self.name)
+
+
+def _client_module():
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
+    return S
+
+
+def test_client_without_server_fails_loudly():
+    L = _client_module()._client_lib()
+    c = ctypes.c_void_p()
+    rc = L.qcc_open(b"/qcart_no_such_server", ctypes.byref(c))
+    assert rc == -7 and not c.value
+    assert b"no step server" in L.qcc_last_error(None)
+
+
+def test_client_calls_through_the_protocol():
+    S = _client_module()
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    srv = MockServer(f"/qcart_mock_{os.getpid()}", P=2, N=8)
+    try:
+        ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=7, omega=3.14159)
+        a = S._ServedSimulation(ph, srv.name)
+        b = S._ServedSimulation(ph, srv.name)
+        with pytest.raises(RuntimeError, match="slots are taken"):
+            S._ServedSimulation(ph, srv.name)
+        assert srv.hdr.n_clients == 2
+        state = (np.arange(8) + 1j).astype(np.complex128)
+        q, xm, fail = a.step(state, 1 / 1440, 0.8, 6.28)
+        assert (q, xm, fail) == (1.5, 0.8, 0) and np.array_equal(state, -(np.arange(8) + 1j))
+        q, xm, fail = b.simulate_10_steps(state, 1 / 1440, -1.6, 6.28)
+        assert (q, xm, fail) == (15.0, -1.6, 1) and np.array_equal(state, np.arange(8) + 1j)
+        a.set_seed(2 ** 32 + 77)                        # the int's low 32 bits, as the reference's MKL_UINT
+        assert srv.slots[0].value == 77.0
+        assert a.x_expectation(state) == float(np.arange(8).sum())
+        with pytest.raises(ValueError, match="required size 8"):
+            a.step(np.zeros(9, np.complex128), 1 / 1440, 0.0, 6.28)
+        # concurrent callers: every call answered with its own slot's data
+        errs = []
+
+        def run(m, sign):
+            st = np.full(8, sign, np.complex128)
+            for _ in range(200):
+                m.step(st, 1 / 1440, 0.0, 6.28)
+            if not np.array_equal(st, np.full(8, sign)):
+                errs.append(sign)
+        ts = [threading.Thread(target=run, args=(m, s)) for m, s in ((a, 1.0), (b, -2.0))]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert not errs
+        a.close()
+        assert srv.slots[0].owner == 0 and srv.hdr.n_clients == 1
+        c = S._ServedSimulation(ph, srv.name)   # the freed slot is claimed again
+        b.close()
+        c.close()
+        # a mismatched module (the drivers' check_settings handshake) is refused
+        with pytest.raises(RuntimeError, match="serves family"):
+            S._ServedSimulation(ph.with_(n_max=15), srv.name)
+    finally:
+        srv.close()

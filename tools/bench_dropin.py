@@ -6,10 +6,15 @@ copies per call): the reference drivers' own call pattern, IHO/main_parallel.py:
 
 --procs: the reference's process model (IHO/main_parallel.py:345-359: 30-40 actor processes, each with its
 own `simulation` module stepping one env): P independent processes, each `install()`ing the drop-in and calling
-`step` on one env, all on the same GPU, started together behind a file barrier; the aggregate is the sum of
-the processes' step calls/s over the common timed window. --kinds gpu,cpu adds the same P processes running the oracle
-(the CPU restatement, one env and one host core each — what the reference's own processes do) for comparison.
-The parent never touches the GPU; each process is a fresh child.
+`step` on one env, started together behind a file barrier. Kinds:
+  gpu     each process its own plain drop-in (its own HIP context, B = 1 launches, copies and syncs per call)
+  server  one StepServer process owns the GPU (qc_server_*); the P processes attach with
+          install(..., server=name) (libqcart_client.so, no HIP in them) and every tick steps all pending envs in
+          one batched launch
+  cpu     the oracle (the CPU restatement, one env and one host core each — what the reference's processes do)
+The aggregate counts every process's step calls inside the COMMON window [latest start, earliest end] (each
+process records its call count after every 80-step control interval; counts at the window edges interpolated)
+divided by that window. The parent never touches the GPU; each process is a fresh child.
 """
 import argparse
 import json
@@ -53,9 +58,10 @@ def worker(args):
     dt, gamma = 1 / 1440, 2 * pi
     state = np.zeros(args.n_max + 1, np.complex128)
     state[0] = 1.0
-    if args.kind == "gpu":
+    if args.kind in ("gpu", "server"):
         from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
-        sim = S.install("inverted_harmonic", device=0, n_max=args.n_max)
+        sim = S.install("inverted_harmonic", device=0, n_max=args.n_max,
+                        server=args.name if args.kind == "server" else None)
         sim.set_seed(1000 + args.rank)
 
         def step(F):
@@ -78,6 +84,7 @@ def worker(args):
     n = 0
     t0 = time.time()
     t_end = t0 + args.seconds
+    marks = [(t0, 0)]
     while True:
         for _ in range(80):                            # one control interval per force
             step(0.8 * ((n // 80) % 3 - 1))
@@ -85,22 +92,54 @@ def worker(args):
         state[:] = 0                                   # restart the episode (keeps the env physical)
         state[0] = 1.0
         t = time.time()
+        marks.append((t, n))
         if t >= t_end:
             break
-    print(json.dumps({"rank": args.rank, "calls": n, "t0": t0, "t1": t}), flush=True)
+    print(json.dumps({"rank": args.rank, "calls": n, "t0": t0, "t1": t, "marks": marks}), flush=True)
+
+
+def serve(args):
+    """The step-server process: owns the GPU, serves until its stdin closes, prints its statistics."""
+    import threading
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
+    srv = S.StepServer("inverted_harmonic", max_clients=args.max_clients, name=args.name, device=0,
+                       batch_wait_us=args.batch_wait_us, n_max=args.n_max)
+
+    def watch():
+        sys.stdin.read()
+        srv.stop()
+    threading.Thread(target=watch, daemon=True).start()
+    print("ready", flush=True)
+    srv.run(0)
+    print(json.dumps(srv.stats()), flush=True)
+    srv.close()
 
 
 def fan_out(args, kind, P):
     go = os.path.join(tempfile.mkdtemp(prefix="qcart_dropin_"), "go")
     env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    server = None
+    name = f"/qcart_bench_{os.getpid()}_{P}"
+    if kind == "server":
+        serr = open(go + ".server_err", "w+")
+        server = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--serve", "--name", name,
+                                   "--max-clients", str(P), "--n-max", str(args.n_max),
+                                   "--batch-wait-us", str(args.batch_wait_us)],
+                                  cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=serr,
+                                  text=True)
+        if not server.stdout.readline().startswith("ready"):
+            server.wait()
+            serr.seek(0)
+            raise RuntimeError(serr.read()[-2000:])
     errs = [open(go + f".err{r}", "w+") for r in range(P)]
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker", "--kind", kind, "--rank", str(r),
-                               "--go", go, "--seconds", str(args.seconds), "--n-max", str(args.n_max)],
+                               "--go", go, "--seconds", str(args.seconds), "--n-max", str(args.n_max),
+                               "--name", name],
                               cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=errs[r], text=True)
              for r in range(P)]
 
     def fail(r):
-        for p in procs:
+        for p in procs + ([server] if server else []):
             if p.poll() is None:
                 p.kill()
         errs[r].seek(0)
@@ -116,12 +155,26 @@ def fan_out(args, kind, P):
         if p.returncode != 0:
             fail(r)
         res.append(json.loads(out.strip().splitlines()[-1]))
-    # the common window: every process was stepping throughout [max t0, min t1]; rates over each process' own
-    # window are summed (each window covers the common one)
-    agg = sum(r["calls"] / (r["t1"] - r["t0"]) for r in res)
-    overlap = min(r["t1"] for r in res) - max(r["t0"] for r in res)
-    return {"kind": kind, "procs": P, "step_calls_per_s": agg, "per_proc_calls_per_s": agg / P,
-            "us_per_call": P / agg * 1e6, "seconds": args.seconds, "overlap_s": overlap}
+    srv_stats = None
+    if server is not None:
+        out, _ = server.communicate(input="", timeout=120)
+        srv_stats = json.loads(out.strip().splitlines()[-1])
+    # the common window [latest start, earliest end]: every process was stepping throughout it; each process's
+    # calls inside it from its per-interval marks (interpolated at the edges)
+    import numpy as np
+    T0, T1 = max(r["t0"] for r in res), min(r["t1"] for r in res)
+    if T1 - T0 < 0.5 * args.seconds:
+        raise RuntimeError(f"the processes overlapped only {T1 - T0:.2f} s of {args.seconds} s")
+    inside = 0.0
+    for r in res:
+        t, n = np.array(r["marks"]).T
+        inside += float(np.interp(T1, t, n) - np.interp(T0, t, n))
+    agg = inside / (T1 - T0)
+    row = {"kind": kind, "procs": P, "step_calls_per_s": agg, "per_proc_calls_per_s": agg / P,
+           "us_per_call": P / agg * 1e6, "seconds": args.seconds, "common_window_s": T1 - T0}
+    if srv_stats:
+        row["server"] = dict(srv_stats, calls_per_tick=srv_stats["calls"] / max(1, srv_stats["ticks"]))
+    return row
 
 
 def main():
@@ -130,13 +183,19 @@ def main():
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--procs", default="")
     ap.add_argument("--seconds", type=float, default=5.0)
-    ap.add_argument("--kinds", default="gpu", help="gpu,cpu: the drop-in and/or the oracle processes")
+    ap.add_argument("--kinds", default="gpu", help="gpu,server,cpu: the plain drop-in / the step server / the oracle")
     ap.add_argument("--out", default="")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--kind", default="gpu")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--go", default="")
+    ap.add_argument("--serve", action="store_true")
+    ap.add_argument("--name", default="")
+    ap.add_argument("--max-clients", type=int, default=16)
+    ap.add_argument("--batch-wait-us", type=float, default=40.0)
     args = ap.parse_args()
+    if args.serve:
+        return serve(args)
     if args.worker:
         return worker(args)
     if not args.procs:

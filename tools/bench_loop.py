@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--capacity", type=int, default=0)   # xp: 7000 x 18 x 100 (IHO/arguments.py:80, main_parallel.py:595)
     ap.add_argument("--input", choices=("xp", "measurements"), default="xp")
+    ap.add_argument("--marker", action="store_true",
+                    help="wrap the timed steps in a roctx range 'timed' (tools/loop_breakdown.py, rocprofv3 --marker-trace)")
     args = ap.parse_args()
     B = args.batch
     meas = args.input == "measurements"
@@ -51,9 +53,12 @@ def main():
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     actor_ms = replay_ms = 0.0
     rows = 0
+    n_done = 0
     for it in range(args.warmup + args.steps):
         if it == args.warmup:
             torch.cuda.synchronize()
+            if args.marker:
+                torch.cuda.nvtx.range_push("timed")
             t0 = time.perf_counter()
             actor_ms = replay_ms = 0.0
             rows = 0
@@ -63,6 +68,8 @@ def main():
         steps_done += B
         obs, reward, done, info = env.step(a)
         rows += int(info["valid"].sum())
+        if it >= args.warmup:
+            n_done += int(done.sum())
         r0.record()
         if meas:
             mem.store(info["rows"], info["valid"])
@@ -77,6 +84,9 @@ def main():
         replay_ms += r0.elapsed_time(r1)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if args.marker:
+        torch.cuda.nvtx.range_pop()
+    done_frac = n_done / (B * args.steps)
     K = args.steps
     net = "DQN_measurement" if meas else "direct_DQN"
     print(json.dumps({"metric": f"actor loop RL steps/s (BatchedEnv IHO N=512 input={args.input} + device {net} actor)",
@@ -85,6 +95,7 @@ def main():
                       "actor_ms_per_control_step": actor_ms / K, "actor_share": actor_ms / (dt * 1e3),
                       "replay_ms_per_control_step": replay_ms / K, "replay_share": replay_ms / (dt * 1e3),
                       "replay_len": len(mem),
+                      "done_fraction_per_control_step": done_frac,
                       "experience_rows_per_s": rows / dt,
                       "row_len": mem.data_size,
                       "data": f"synthetic: |0> resets, random-initialised {net} weights"}), flush=True)

@@ -17,7 +17,7 @@ torch = pytest.importorskip("torch")
 from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg  # noqa: E402
 from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S  # noqa: E402
 
-import test_gpu_noise as TN  # noqa: E402
+from tests import test_gpu_noise as TN  # noqa: E402
 
 _N = [0]
 

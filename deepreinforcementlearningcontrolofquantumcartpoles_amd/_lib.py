@@ -40,7 +40,7 @@ EXPORTS = (
     "qc_replay_store_xp", "qc_replay_sample", "qc_replay_update", "qc_replay_rebuild", "qc_replay_stats",
     "qc_replay_buffers", "qc_set_seed_mt19937_envs",
     "qc_server_create", "qc_server_run", "qc_server_stop", "qc_server_stats", "qc_server_last_error",
-    "qc_server_destroy",
+    "qc_server_destroy", "qc_env_tail",
 )
 
 
@@ -64,6 +64,34 @@ class QcParams(ctypes.Structure):
         ("env_offset", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
         ("xth", ctypes.c_double),
+    ]
+
+
+class QcEnvTailArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int64),
+        ("kind", ctypes.c_int32),
+        ("n_obs", ctypes.c_int32),
+        ("interval", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+        ("dt", ctypes.c_double),
+        ("xth", ctypes.c_double),
+        ("input_scaling", ctypes.c_double),
+        ("failing_reward", ctypes.c_double),
+        ("fail_step", ctypes.c_void_p),
+        ("term_step", ctypes.c_void_p),
+        ("obs", ctypes.c_void_p),
+        ("pending", ctypes.c_void_p),
+        ("t", ctypes.c_void_p),
+        ("steps", ctypes.c_void_p),
+        ("episode_return", ctypes.c_void_p),
+        ("obs32", ctypes.c_void_p),
+        ("reward", ctypes.c_void_p),
+        ("done", ctypes.c_void_p),
+        ("valid", ctypes.c_void_p),
+        ("fin", ctypes.c_void_p),
+        ("fin_cap", ctypes.c_int64),
+        ("fin_n", ctypes.c_void_p),
     ]
 
 
@@ -171,6 +199,7 @@ def lib() -> ctypes.CDLL:
     L.qc_env_counters.argtypes = [vp, vp, vp]
     L.qc_set_seed_mt19937.argtypes = [vp, vp]
     L.qc_set_seed_mt19937_envs.argtypes = [vp, vp, vp]
+    L.qc_env_tail.argtypes = [vp, P(QcEnvTailArgs)]
     L.qc_server_create.argtypes = [P(QcParams), ctypes.c_int, i32, ctypes.c_char_p, d, P(vp)]
     L.qc_server_run.argtypes = [vp, d]
     L.qc_server_stop.argtypes = [vp]

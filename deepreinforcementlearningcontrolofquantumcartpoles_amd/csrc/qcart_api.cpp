@@ -859,6 +859,43 @@ int qc_group_layout(qc_handle* h, int32_t* order, int64_t order_len, int32_t* mi
     return h->d_order_mixed ? (int)h->acts.size() : 0;
 }
 
+int qc_env_tail(qc_handle* h, const qc_env_tail_args* in) {
+    if (!h || !in) return QC_EINVAL;
+    const qc_env_tail_args& x = *in;
+    if (x.B != h->p.batch) return fail(h, QC_EINVAL, "env tail: B must be the handle's batch");
+    if (x.kind != QC_IHO && x.kind != QC_IQO) return fail(h, QC_EINVAL, "env tail: the cartpole families (IHO, IQO)");
+    if (x.kind == QC_IQO && !x.term_step) return fail(h, QC_EINVAL, "env tail: IQO needs term_step");
+    if (x.B > 0 && (!x.fail_step || !x.obs || !x.pending || !x.t || !x.steps || !x.episode_return || !x.reward ||
+                    !x.done || !x.valid || !x.fin || !x.fin_n || x.fin_cap < 1 || x.n_obs < 1 || x.interval < 1))
+        return fail(h, QC_EINVAL, "env tail: missing buffer or bad size");
+    EnvTailArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = x.B;
+    a.kind = x.kind;
+    a.n_obs = x.n_obs;
+    a.interval = x.interval;
+    a.dt = x.dt;
+    a.xth = x.xth;
+    a.input_scaling = x.input_scaling;
+    a.failing_reward = x.failing_reward;
+    a.fail_step = x.fail_step;
+    a.term_step = x.term_step;
+    a.obs = x.obs;
+    a.pending = x.pending;
+    a.t = x.t;
+    a.steps = x.steps;
+    a.episode_return = x.episode_return;
+    a.obs32 = x.obs32;
+    a.reward = x.reward;
+    a.done = x.done;
+    a.valid = x.valid;
+    a.fin = x.fin;
+    a.fin_cap = x.fin_cap;
+    a.fin_n = x.fin_n;
+    DeviceGuard g(h->device);
+    return launch_env_tail(a, h->stream) ? fail(h, QC_EHIP, "env tail kernel launch failed") : QC_OK;
+}
+
 int qc_take_errors(qc_handle* h) {
     if (!h) return QC_EINVAL;
     DeviceGuard g(h->device);

@@ -149,6 +149,28 @@ int launch_record(const RecArgs& a, void* stream);
 int launch_wavefunction(const void* psi, int precision, int64_t B, int32_t N, int32_t lo, int32_t cnt, double scaling,
                         float* out, void* stream);
 
+// the batched episode loop's bookkeeping (qcart_env.hip, qc_env_tail): see qc_env_tail_args in qcart.h
+struct EnvTailArgs {
+    int64_t B;
+    int32_t kind, n_obs, interval, pad;
+    double dt, xth, input_scaling, failing_reward;
+    const int32_t* fail_step;
+    const int32_t* term_step;
+    const double* obs;
+    uint8_t* pending;
+    double* t;
+    int64_t* steps;
+    double* episode_return;
+    float* obs32;
+    float* reward;
+    uint8_t* done;
+    uint8_t* valid;
+    double* fin;
+    int64_t fin_cap;
+    int64_t* fin_n;
+};
+int launch_env_tail(const EnvTailArgs& a, void* stream);
+
 // reference noise stream (qcart_noise.hip): per-env MT19937 state [B][kMtWords] uint32 (624 words,
 // the read index, one pad word)
 constexpr int kMtWords = 626;

@@ -1362,6 +1362,23 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         __syncthreads();
     }
     if (!active) return;
+    // the env's steps this call: min(n_steps, its budget)
+    auto steps_of = [&]() {
+        int n = a.n_steps;
+        if (a.env_steps) {
+            const int e = a.env_steps[env];
+            n = e < 0 ? 0 : (e < n ? e : n);
+        }
+        return __builtin_amdgcn_readfirstlane(n);
+    };
+    // a frozen env (no step budget: the not-finished envs of a reset interval) with no observation or
+    // termination index requested is only reported (fail_step 0): its psi is neither read nor written (fp64
+    // kernels; the fp32 R = 32 kernels sit at their register limit, where the extra exit moved their spills)
+    constexpr bool FROZEN_SKIP = sizeof(RT) == 8;
+    if (FROZEN_SKIP && !a.obs_out && !a.term_step && steps_of() == 0) {
+        if (lane == 0 && a.fail_step) a.fail_step[env] = 0;
+        return;
+    }
     const int base = gl * R;
     const int lnv = lane;   // the lane argument of the stencil / reduction / solve helpers
     const int N = a.N;
@@ -1431,12 +1448,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     constexpr bool NZL = MODE >= 1 && sizeof(RT) == 8 && QCART_NZ_LDS;
     double nz0 = 0.0, nz1 = 0.0;
 
-    int n_my = a.n_steps;
-    if (a.env_steps) {
-        const int e = a.env_steps[env];
-        n_my = e < 0 ? 0 : (e < n_my ? e : n_my);
-    }
-    n_my = __builtin_amdgcn_readfirstlane(n_my);
+    const int n_my = steps_of();
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
@@ -2030,8 +2042,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         for (int j = 0; j < R; ++j) psi[j] = C(psi[j].re * (RT)scl, psi[j].im * (RT)scl);   // normalised
     }
     // write back (row indices recomputed from an opaque lane copy: kept from the loads, they were spilled
-    // across the loop)
-    {
+    // across the loop); a frozen env's psi is unchanged (scl = 1): not written
+    if (!FROZEN_SKIP || n_my > 0) {
         int wb = gl * R;
         asm volatile("" : "+v"(wb));
 #pragma unroll

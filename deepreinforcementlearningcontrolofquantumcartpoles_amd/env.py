@@ -24,9 +24,23 @@ the observation is get_data_wavefunction(state) * input_scaling: float32 hstack(
 (HO, IHO; IHO/main_parallel.py:143-151,270-309) the observation is the device measurement record
 [B][2][read_length] (measurements.MeasurementRecord, updated in place by the qc_record kernel) and the
 experience rows [B][row_len] come from the same kernel (info['rows']).
+
+Auto-reset modes (cartpoles, 'xp' input):
+  * reset="immediate" (default): a finished env is reset and runs its zero-force first interval inside the same
+    step() call, so the returned obs of a done env is already the next episode's first observation (the terminal
+    one is info['terminal_obs']) — the reference actor's own interleaving; one more (partial) step launch and a few
+    host synchronisations per call.
+  * reset="deferred": a finished env returns its terminal obs and runs its reset interval (|0> / the IQO packet at
+    F = 0) in the NEXT call, inside the same step launch as the other envs (its action of that call is ignored,
+    info['reset'] marks it, no valid transition); the per-control-step bookkeeping (reward, done, return, episode
+    time, the finished-episode ring) is one device kernel (qc_env_tail) and the call never synchronises with the
+    host. Every env's own sequence — reset, zero-force interval, decisions on its observations, per-env noise — is
+    the immediate mode's (tests/test_gpu_env.py: per-env episodes bitwise equal); only the calls they fall in
+    differ, and every call advances every env exactly one control interval.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -41,7 +55,8 @@ class BatchedEnv:
                  env_offset: int = 0, input_scaling: float = 1.0, failing_reward: float = -1.0,
                  reward_multiply: float = 1.0, t_max: float = 100.0, phonon_cutoff: float = 20.0,
                  energy_cutoff: float = 12.0, init_energy_cutoff: float = 7.5, auto_reset: bool = True,
-                 reset_kind: str = "reference", input: str = "xp", read_length: Optional[int] = None):
+                 reset_kind: str = "reference", input: str = "xp", read_length: Optional[int] = None,
+                 reset: str = "immediate"):
         self.ph = physics
         self.B = int(batch)
         self.st = Stepper(physics, self.B, device, seed=seed, env_offset=env_offset)
@@ -67,6 +82,13 @@ class BatchedEnv:
         if input == "measurements" and not physics.fock:
             raise ValueError("the 'measurements' input exists for the Fock families (HO, IHO) only")
         self.input = input
+        if reset not in ("immediate", "deferred"):
+            raise ValueError("reset must be 'immediate' or 'deferred'")
+        if reset == "deferred" and not (self.cartpole and input == "xp" and auto_reset):
+            raise ValueError("reset='deferred' is built for the cartpoles (IHO, IQO) with the 'xp' input and auto_reset")
+        self.reset_mode = reset
+        self._pending = torch.zeros(self.B, dtype=torch.uint8, device=self.dev)
+        self._calls = 0
         self.rec = None
         if input == "measurements":
             self.rec = MeasurementRecord(self.st, read_length, input_scaling=input_scaling)
@@ -168,6 +190,7 @@ class BatchedEnv:
         if mask is None:
             mask = torch.ones(self.B, dtype=torch.bool, device=self.dev)
         mask = mask.to(device=self.dev, dtype=torch.bool)
+        self._pending.masked_fill_(mask, 0)   # (reset='deferred': a pending reset is done here instead)
         self._reset_states(mask)
         self.t = torch.where(mask, torch.zeros_like(self.t), self.t)
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
@@ -209,11 +232,51 @@ class BatchedEnv:
         return self.obs
 
     # ------------------------------------------------------------------ step
+    def _step_deferred(self, actions: torch.Tensor):
+        """reset='deferred': the envs finished in the previous call take their reset interval now (reset kernel +
+        the zero force in the same step launch), then qc_env_tail does the bookkeeping on the device."""
+        from . import _lib as L
+        fam = self.ph.family
+        pend = self._pending
+        reset_now = pend.clone().view(torch.bool)
+        if fam == cfg.IHO:
+            self.st.reset(self.psi, 0, mask=pend)
+        else:
+            self.st.reset(self.psi, 2, mask=pend, arg0=0.0, arg1=0.0, arg2=1.0)
+        acts = torch.where(reset_now, torch.full_like(actions, self.half), actions)
+        out = self.st.step(self.psi, acts, self.ci, want_fail=True, want_obs=True, want_term=(fam == cfg.IQO))
+        B, n = self.B, self.st.n_obs
+        obs = torch.empty((B, n), dtype=torch.float32, device=self.dev)
+        reward = torch.empty(B, dtype=torch.float32, device=self.dev)
+        done = torch.empty(B, dtype=torch.uint8, device=self.dev)
+        valid = torch.empty(B, dtype=torch.uint8, device=self.dev)
+        p = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+        a = L.QcEnvTailArgs(B=B, kind=fam, n_obs=n, interval=self.ci, dt=self.ph.dt, xth=self.ph.xth,
+                            input_scaling=self.input_scaling, failing_reward=self.failing_reward,
+                            fail_step=p(out["fail_step"]), term_step=p(out.get("term_step")), obs=p(out["obs"]),
+                            pending=p(pend), t=p(self.t), steps=p(self.steps), episode_return=p(self.episode_return),
+                            obs32=p(obs), reward=p(reward), done=p(done), valid=p(valid), fin=p(self._fin),
+                            fin_cap=self._fin_cap, fin_n=p(self._fin_n))
+        self.st._bind_stream()
+        L.check(L.lib().qc_env_tail(self.st._h, ctypes.byref(a)), self.st._h)
+        last_obs = self.obs
+        self.obs = obs
+        self.last_action = acts
+        self._calls += 1
+        if self._calls % 16 == 0:   # deferred action-range errors, at most 16 calls late (synchronises)
+            self.st.check()
+        done_b = done.view(torch.bool)
+        info = {"valid": valid.view(torch.bool), "reset": reset_now, "t": self.t.clone(), "last_obs": last_obs,
+                "fail_step": out["fail_step"], "numerical_failure": done_b & (out["fail_step"] > 0)}
+        return obs, reward, done_b, info
+
     def step(self, actions: torch.Tensor):
         """Apply per-env actions for one control interval. Returns (obs, reward, done, info):
         reward is the reference's stored reward-row value, info['valid'] marks transitions the
         reference would store, info['numerical_failure'] the Fail-terminated episodes."""
         actions = actions.to(device=self.dev, dtype=torch.int32).contiguous()
+        if self.reset_mode == "deferred":
+            return self._step_deferred(actions)
         last_obs = self.obs
         fam = self.ph.family
         out = self.st.step(self.psi, actions, self.ci, want_fail=True, want_obs=True,

@@ -416,6 +416,39 @@ int qc_replay_stats(qc_replay* r, qc_replay_stats_t* out);
 /* device pointers of the tree and the row storage (introspection, tests) */
 int qc_replay_buffers(const qc_replay* r, const double** tree, const float** data);
 
+/* ---- batched episode loop: the per-control-step bookkeeping of Control.do_episode --------------------------
+ * (IHO/main_parallel.py:242-268, IQO/main_parallel.py:190-221; the cartpoles, 'xp' input) for every env after a
+ * step call of one control interval, on the device (BatchedEnv reset="deferred"): pending[e] (in) marks the envs
+ * whose call was their reset interval (the zero-th step without control): their time restarts at one interval,
+ * return at 0, no valid transition; an episode over at that first control step is reported with return 0 (the
+ * i != control_interval guard, IHO:250). Other envs: t += interval dt, done = Fail in the interval or out of
+ * bounds (IHO |<x>| > xth: |obs[e][0]| > xth; IQO: term_step[e] >= 0), reward failing_reward / 1, valid,
+ * return += reward. Done envs: (return, t) appended to the ring fin [2][fin_cap + 1] at *fin_n (env order; the
+ * reference's result queue, IHO:300-327) and pending[e] (out) = 1: they reset in the next call. All device
+ * pointers; obs32 [B][n_obs] = float(obs) * input_scaling (NULL: skip). No host synchronisation. */
+typedef struct qc_env_tail_args {
+    int64_t B;
+    int32_t kind;             /* enum qc_family of the cartpole: QC_IHO or QC_IQO */
+    int32_t n_obs, interval;  /* observables per env; physics steps per control interval */
+    int32_t pad;
+    double dt, xth, input_scaling, failing_reward;
+    const int32_t* fail_step; /* [B] qc_step's fail_step */
+    const int32_t* term_step; /* [B] qc_step's term_step (IQO) or NULL */
+    const double* obs;        /* [B][n_obs] qc_step's obs_out */
+    uint8_t* pending;         /* [B] in: reset interval in this call; out: resets in the next call */
+    double* t;                /* [B] episode time */
+    int64_t* steps;           /* [B] physics steps of the episode */
+    double* episode_return;   /* [B] */
+    float* obs32;             /* [B][n_obs] or NULL */
+    float* reward;            /* [B] the reference's reward-row value */
+    uint8_t* done;            /* [B] */
+    uint8_t* valid;           /* [B] transitions the reference stores */
+    double* fin;              /* [2][fin_cap + 1] finished (return, length) */
+    int64_t fin_cap;
+    int64_t* fin_n;           /* [1] episodes appended so far */
+} qc_env_tail_args;
+int qc_env_tail(qc_handle* h, const qc_env_tail_args* a);
+
 /* ---- step server: the reference's process model on one GPU ------------------------------------------------
  * The drivers run 30-40 actor processes, each with its own `simulation` module stepping ONE env per call
  * (IHO/main_parallel.py:345-359, :264). A step server owns one handle of batch max_clients (env e = client slot

@@ -98,3 +98,22 @@ def test_client_library_exports_every_declared_symbol():
         assert hasattr(L, s), s
     deps = subprocess.run(["ldd", CLIENT], capture_output=True, text=True).stdout
     assert "amdhip" not in deps and "hsa" not in deps
+
+
+def test_env_tail_args_struct_matches_header(tmp_path):
+    """_lib.QcEnvTailArgs mirrors qc_env_tail_args (field order, offsets, size) compiled against the header."""
+    import shutil
+    import subprocess
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    names = [f[0] for f in _lib.QcEnvTailArgs._fields_]
+    src = tmp_path / "tail.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "qcart.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(qc_env_tail_args, {n}));\n' for n in names)
+                   + 'printf("%zu\\n", sizeof(qc_env_tail_args));return 0;}\n')
+    exe = tmp_path / "tail"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [getattr(_lib.QcEnvTailArgs, n).offset for n in names] + [ctypes.sizeof(_lib.QcEnvTailArgs)]
+    assert got == want

@@ -216,3 +216,73 @@ def test_out_of_range_actions_raise_at_the_next_check():
         st.step_kernel_time()
     assert torch.isfinite(torch.view_as_real(psi)).all()
 
+
+
+def _episodes_per_env(mode, ph, B, calls, policy):
+    """Each env's finished episodes (return, length, first-interval flag) in its own order, and the ring."""
+    env = BatchedEnv(ph, B, 0, seed=5, reset=mode)
+    env.reset()
+    per = [[] for _ in range(B)]
+    for _ in range(calls):
+        obs, rew, done, info = env.step(policy(env.obs))
+        d = done.cpu().numpy()
+        if not d.any():
+            continue
+        if mode == "immediate":
+            ret, ln = info["episode_return"].cpu().numpy(), info["episode_length"].cpu().numpy()
+        else:
+            ret, ln = env.episode_return.cpu().numpy(), env.t.cpu().numpy()
+        for e in np.nonzero(d)[0]:
+            per[e].append((float(ret[e]), float(ln[e])))
+    return per, env
+
+
+@pytest.mark.parametrize("fam", [cfg.IHO, cfg.IQO])
+def test_deferred_reset_keeps_every_envs_episodes(fam):
+    """reset='deferred' (a finished env takes its reset interval in the next call, inside the same step launch,
+    bookkeeping on the device by qc_env_tail, no host sync): every env's own episode sequence — returns and
+    lengths — is bitwise the immediate mode's (per-env noise keyed by the env's own step count, a policy of the
+    observations only), just spread over more calls."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=127) if fam == cfg.IHO else cfg.DEFAULTS[cfg.IQO].with_(x_max=12.8)
+    B = 24
+
+    def policy(obs):   # a deterministic bad controller: pushes the pole the way it leans (episodes end)
+        return torch.where(obs[:, 0] > 0, 20, 0).to(torch.int32)
+    imm, _ = _episodes_per_env("immediate", ph, B, 40, policy)
+    dfr, env = _episodes_per_env("deferred", ph, B, 48, policy)
+    n = 0
+    for e in range(B):
+        k = min(len(imm[e]), len(dfr[e]))
+        assert imm[e][:k] == dfr[e][:k], e
+        n += k
+    assert n >= B   # every env finished at least one episode in both runs
+    # the ring holds the same episodes as the per-call done flags, in env order per call
+    fr = env.finished_returns
+    assert sum(r.numel() for r, _ in fr) == sum(len(x) for x in dfr)
+
+
+def test_deferred_reset_call_semantics():
+    """The call after an env finished: its action is ignored (zero force: the reset interval), info['reset']
+    marks it, its transition is not valid, its time restarts at one interval and its return at 0; the done env
+    itself returned its terminal observation, and rewards / validity of the others are the reference's."""
+    ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=127)
+    B = 16
+    env = BatchedEnv(ph, B, 0, seed=3, reset="deferred")
+    env.reset()
+    push = torch.full((B,), 20, dtype=torch.int32, device="cuda")
+    prev_done = torch.zeros(B, dtype=torch.bool, device="cuda")
+    seen = 0
+    for _ in range(40):
+        obs, rew, done, info = env.step(push)
+        assert torch.equal(info["reset"], prev_done)
+        assert torch.equal(info["valid"], ~prev_done)
+        ci_t = torch.full_like(env.t, ph.control_interval * ph.dt)
+        assert torch.equal(env.t[prev_done], ci_t[prev_done])
+        live = ~prev_done
+        assert torch.equal(rew[live] == -1, done[live]) and bool(torch.all((rew[live] == 1) | (rew[live] == -1)))
+        # a done env's returned obs is its terminal one: out of bounds or Fail
+        oob = obs[:, 0].abs() > ph.xth
+        assert bool(torch.all(oob[done & live] | (info["fail_step"][done & live] > 0)))
+        seen += int((done & live).sum())
+        prev_done = done.clone()
+    assert seen >= B

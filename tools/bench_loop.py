@@ -33,13 +33,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--capacity", type=int, default=0)   # xp: 7000 x 18 x 100 (IHO/arguments.py:80, main_parallel.py:595)
     ap.add_argument("--input", choices=("xp", "measurements"), default="xp")
+    ap.add_argument("--reset", choices=("immediate", "deferred"), default="immediate",
+                    help="BatchedEnv auto-reset mode (deferred: finished envs reset in the next call's launch, no host sync)")
     ap.add_argument("--marker", action="store_true",
                     help="wrap the timed steps in a roctx range 'timed' (tools/loop_breakdown.py, rocprofv3 --marker-trace)")
     args = ap.parse_args()
     B = args.batch
     meas = args.input == "measurements"
     ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)
-    env = BatchedEnv(ph, B, 0, seed=1, input=args.input)
+    env = BatchedEnv(ph, B, 0, seed=1, input=args.input, reset=args.reset)
     if meas:
         actor = MeasurementActor({k: v.cuda() for k, v in random_dqn_measurement(seed=1).items()}, max_batch=B, seed=2)
         row_len = int(env.rows.shape[1])
@@ -49,48 +51,58 @@ def main():
         mem = PrioritizedReplay(args.capacity or 7000 * 18 * 100, 2 * 5 + 2, "random", 0.2, device=0, seed=3)
     obs = env.reset()
     steps_done = 0
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    actor_ms = replay_ms = 0.0
-    rows = 0
-    n_done = 0
+    ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+    marks = []                                          # (actor start, end, replay start, end) per timed step
+    rows = torch.zeros((), dtype=torch.int64, device="cuda")
+    n_done = torch.zeros((), dtype=torch.int64, device="cuda")
+    # no host synchronisation inside the timed loop (device counters, events read afterwards): the loop's own
+    # cost is what the GPU sees
     for it in range(args.warmup + args.steps):
         if it == args.warmup:
             torch.cuda.synchronize()
             if args.marker:
                 torch.cuda.nvtx.range_push("timed")
             t0 = time.perf_counter()
-            actor_ms = replay_ms = 0.0
-            rows = 0
-        e0.record()
+            rows.zero_()
+            n_done.zero_()
+        m = [ev(), ev(), ev(), ev()]
+        m[0].record()
         a = actor.act(obs, eps=DQNActor.eps_threshold(steps_done))
-        e1.record()
+        m[1].record()
         steps_done += B
         obs, reward, done, info = env.step(a)
-        rows += int(info["valid"].sum())
-        if it >= args.warmup:
-            n_done += int(done.sum())
-        r0.record()
+        rows += info["valid"].sum()
+        n_done += done.sum()
+        m[2].record()
         if meas:
             mem.store(info["rows"], info["valid"])
         else:
-            mem.store_xp(info["last_obs"], obs, a, reward, info["valid"])
+            # the row of a done env holds its terminal observation (IHO/main_parallel.py:250-257); in the immediate
+            # mode the returned obs of a done env is already the next episode's
+            nxt = torch.where(done[:, None], info["terminal_obs"], obs) if "terminal_obs" in info else obs
+            mem.store_xp(info["last_obs"], nxt, a, reward, info["valid"])
         smp = mem.obtain_sample(512) if it > 0 else None
         if smp is not None:
             mem.batch_update(smp[0], torch.rand(512, device="cuda"))
-        r1.record()
-        r1.synchronize()
-        actor_ms += e0.elapsed_time(e1)
-        replay_ms += r0.elapsed_time(r1)
+        m[3].record()
+        if it >= args.warmup:
+            marks.append(m)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if args.marker:
         torch.cuda.nvtx.range_pop()
-    done_frac = n_done / (B * args.steps)
+    actor_ms = sum(m[0].elapsed_time(m[1]) for m in marks)
+    replay_ms = sum(m[2].elapsed_time(m[3]) for m in marks)
+    rows = int(rows)
+    done_frac = int(n_done) / (B * args.steps)
     K = args.steps
     net = "DQN_measurement" if meas else "direct_DQN"
-    print(json.dumps({"metric": f"actor loop RL steps/s (BatchedEnv IHO N=512 input={args.input} + device {net} actor)",
+    print(json.dumps({"metric": f"actor loop RL steps/s (BatchedEnv IHO N=512 input={args.input} reset={args.reset} + device {net} actor)",
                       "value": B * K / dt, "unit": "decisions/s", "env_steps_per_s": B * K * ph.control_interval / dt,
+                      # physics env-steps actually taken: the immediate mode adds the reset intervals of the envs
+                      # finished in each call (deferred: they are among the B per call)
+                      "physics_env_steps_per_s": (B * K + (int(n_done) if args.reset == "immediate" else 0))
+                      * ph.control_interval / dt,
                       "batch": B, "control_steps": K, "ms_per_control_step": dt / K * 1e3,
                       "actor_ms_per_control_step": actor_ms / K, "actor_share": actor_ms / (dt * 1e3),
                       "replay_ms_per_control_step": replay_ms / K, "replay_share": replay_ms / (dt * 1e3),

@@ -21,6 +21,9 @@ using namespace qcart;
 
 namespace {
 constexpr int kMaxSlots = 64;
+// qc_step calls of at most this many physics steps on at most this many envs read their tables from L2 (MODE 0)
+constexpr int kShortCallSteps = 10;
+constexpr int64_t kShortCallBatch = 4096;
 std::mutex g_err_mu;
 std::string g_create_err;
 
@@ -568,6 +571,19 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
     a.fail_step = fail_step;
     a.term_step = term_step;
     a.obs_out = obs_out;
+    // short calls on small batches (the drop-in's step / simulate_10_steps, the step server's ticks): the factor
+    // tables are read from the slot blocks in L2 by each wave (MODE 0) — no per-workgroup LDS image of the slot
+    // (120 KiB at IHO N = 512) for one or ten steps, and no slot-grouping launch (each wave has its own slot).
+    // QCART_SHORT_MODE0=0 turns it off (A/B)
+    {
+        static const bool short_mode0 = !(std::getenv("QCART_SHORT_MODE0") && std::atoi(std::getenv("QCART_SHORT_MODE0")) == 0);
+        if (short_mode0 && n_steps <= kShortCallSteps && h->p.batch <= kShortCallBatch && a.tab_mode != 0) {
+            a.tab_mode = 0;
+            a.lds_bytes = 0;
+            a.lds_img = 0;
+            a.lds_nz = 0;
+        }
+    }
     // grid moment orders above the step kernel's fused epilogue: the observation kernel runs after the step
     const bool obs_after = obs_out && !h->op.fock && h->p.moment_order > kStepMaxMomentOrder;
     if (obs_after) a.obs_out = nullptr;
@@ -590,7 +606,7 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
         noise = h->d_noise;
     }
     a.noise = noise;
-    if (actions || env_steps) {
+    if ((actions || env_steps) && a.tab_mode != 0) {
         // group envs by force slot, padded to whole workgroups: every workgroup then shares one slot's
         // tables (the per-block LDS image); envs without a step budget form a last group of their own
         // (a reset interval of a few finished envs then costs in proportion to them); order within a

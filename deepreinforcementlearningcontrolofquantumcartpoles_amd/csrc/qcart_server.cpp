@@ -88,6 +88,8 @@ struct qc_server {
     double cur_dt = 0, cur_gamma = 0;
     std::atomic<int> stop{0};
     int64_t ticks = 0, calls = 0;
+    // per-tick phase sums (us): batching wait, host launches, GPU until the stream sync returned, publishing
+    double t_wait = 0, t_launch = 0, t_gpu = 0, t_publish = 0;
 };
 
 namespace {
@@ -135,6 +137,7 @@ void free_server(qc_server* s) {
 
 // one tick over the pending slots `pend`
 void serve_tick(qc_server* s, const std::vector<int>& pend) {
+    const double t_start = now_us();
     const int P = s->P, N = s->N;
     struct Req { int op, n; uint32_t seed; double dt, force, gamma; };
     std::vector<Req> rq(P);
@@ -216,11 +219,15 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         const int rc = qc_moments(s->h, s->d_psi, s->d_obs);
         if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op >= QCS_OP_MOMENTS) es.push_back(e); err_all(es, rc); }
     }
+    const double t_l = now_us();
     if (hipStreamSynchronize(s->stream) != hipSuccess) {
         qc_sync(s->h);
         err_all(pend, QC_EHIP);
     }
     if (qc_take_errors(s->h) != 0) err_all(pend, QC_EINVAL);
+    const double t_g = now_us();
+    s->t_launch += t_l - t_start;
+    s->t_gpu += t_g - t_l;
     for (int e : pend) {
         qcs_slot& sl = s->slots[e];
         const Req& r = rq[e];
@@ -246,6 +253,7 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         s->served[e] = __atomic_load_n(&sl.req, __ATOMIC_RELAXED);
         __atomic_store_n(&sl.done, s->served[e], __ATOMIC_SEQ_CST);
     }
+    s->t_publish += now_us() - t_g;
     s->ticks++;
     s->calls += (int64_t)pend.size();
     s->hdr->ticks = (uint64_t)s->ticks;
@@ -376,6 +384,7 @@ int qc_server_run(qc_server* s, double seconds) {
             for (int i = 0; i < 32; ++i) cpu_relax();
             scan(s, pend, owned);
         }
+        s->t_wait += now_us() - t0;
         serve_tick(s, pend);
         idle_since = now_us();
     }
@@ -393,6 +402,15 @@ int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls) {
     if (!s) return QC_EINVAL;
     if (ticks) *ticks = s->ticks;
     if (calls) *calls = s->calls;
+    return QC_OK;
+}
+
+int qc_server_timing(const qc_server* s, double* out) {
+    if (!s || !out) return QC_EINVAL;
+    out[0] = s->t_wait;
+    out[1] = s->t_launch;
+    out[2] = s->t_gpu;
+    out[3] = s->t_publish;
     return QC_OK;
 }
 

@@ -336,7 +336,11 @@ class StepServer:
     def stats(self):
         t, c = ctypes.c_int64(), ctypes.c_int64()
         self._L.qc_server_stats(self._h, ctypes.byref(t), ctypes.byref(c))
-        return {"ticks": t.value, "calls": c.value}
+        tm = (ctypes.c_double * 4)()
+        self._L.qc_server_timing(self._h, tm)
+        n = max(1, t.value)
+        return {"ticks": t.value, "calls": c.value, "us_per_tick": {
+            "batch_wait": tm[0] / n, "launch": tm[1] / n, "gpu": tm[2] / n, "publish": tm[3] / n}}
 
     def close(self):
         if getattr(self, "_h", None):

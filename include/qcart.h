@@ -465,6 +465,9 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
 int qc_server_run(qc_server* s, double seconds);
 int qc_server_stop(qc_server* s);
 int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls);
+/* out[4]: microseconds summed over the ticks — batching wait, host launches, GPU (until the stream sync
+ * returned), publishing the results */
+int qc_server_timing(const qc_server* s, double* out);
 const char* qc_server_last_error(const qc_server* s);
 /* marks the object dead (waiting clients fail with QCC_ENOSERVER) and unlinks it */
 void qc_server_destroy(qc_server* s);

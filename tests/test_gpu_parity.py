@@ -506,7 +506,8 @@ def test_group_layout_packs_slots(B):
     st = Stepper(ph, B, 0, seed=1)
     psi = st.new_state()
     st.reset(psi, 1, arg0=4)
-    st.step(psi, torch.from_numpy(acts).cuda(), 2, env_steps=torch.from_numpy(budget).cuda())
+    # (12 steps: calls of <= 10 steps on small batches read their tables from L2 without grouping, qc_step)
+    st.step(psi, torch.from_numpy(acts).cuda(), 12, env_steps=torch.from_numpy(budget).cuda())
     order, mixed = st.group_layout()
     g = order.shape[1]
     mixed = np.array([wg for wg in mixed if (wg >= 0).any()]).reshape(-1, g)

@@ -312,6 +312,7 @@ KArgs base_args(const qc_handle* h) {
     a.kf = h->d_kf;
     a.kb = h->d_kb;
     a.force = h->d_force;
+    a.bad = h->d_bad;
     return a;
 }
 

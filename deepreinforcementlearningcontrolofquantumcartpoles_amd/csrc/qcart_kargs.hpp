@@ -125,6 +125,7 @@ struct KArgs {
     // sqrt(dt) beta and the Horner ratios a2/a5, a3/a5, a4/a5 — each the same fp64 expression as before
     double inv_sdt, inv_dt, k_hisdt, k_qisdt, k_hidt, k_qidt, k_qdt, k_qsdt, k_dz, k_sb, b2, b3, b4;
     double x2h;                // IHO: -1/omega, X^2's +-2 bands as a multiple of H's (k_step X2H)
+    int32_t* bad;              // the handle's error word: an out-of-range action of an ungrouped call (MODE 0)
 };
 
 // measurement-record update (qcart_record.hip, qc_record)

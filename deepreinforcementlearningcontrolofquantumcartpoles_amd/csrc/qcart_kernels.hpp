@@ -1269,7 +1269,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // a block shares its first env's slot)
     const bool per_wave = MODE == 0 || MODE == 3;
     int slot = a.actions ? a.actions[(!per_wave || !active) ? e0 : env] : a.default_action;
-    slot = clamp_slot(__builtin_amdgcn_readfirstlane(slot));   // never index out of the tables
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    // ungrouped calls (MODE 0 without k_group, qc_step's short calls): an out-of-range action of an env with a step
+    // budget raises the handle's error word here (k_group does it for grouped calls)
+    if (MODE == 0 && a.bad && active && (slot < 0 || slot >= a.n_slots) && lane == 0 &&
+        (!a.env_steps || (a.env_steps[env] > 0 && a.n_steps > 0)))
+        a.bad[0] = 1;
+    slot = clamp_slot(slot);   // never index out of the tables
     // MODE 3: the block's two slots (its first env's and its last env's) and this wave's image
     int slotA = slot, slotB = slot;
     uint32_t img_off = 0;

@@ -1458,7 +1458,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
-    constexpr bool KAR = !(FAM == 2 && R >= 17) && !(sizeof(RT) == 4 && R >= 32);
+    constexpr bool KAR = !(FAM == 2 && R >= 17);
     // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
     // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
@@ -1478,8 +1478,8 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         // the scalar cache; the opaque pointer keeps the compiler from hoisting them) instead of held in SGPRs
         // across the loop: at 106 SGPRs the metric kernel spilled ~90 of them into VGPR lanes (v_writelane /
         // v_readlane on the VALU every step) and 3 VGPRs to scratch; now 92 SGPRs, no spill (loop 2 880 ->
-        // 2 774 instructions). Not for the kernels that spill VGPRs to scratch anyway (grid R = 17, fp32
-        // R = 32), where the per-step loads cost more than they save (C3 198 -> 218 ms per episode)
+        // 2 774 instructions). The fp32 R = 32 kernel (C5) too (round 5: SGPR-spill lane moves 402 -> 112 per
+        // step, 42.5 -> 41.9 ms, same call); not the grid R = 17 kernel (C3: 156.8 -> 159.5 ms, same call)
         const auto& a = step_kargs<KAR>(a_in);   // (shadows the parameter inside the step)
         const double dt = a.dt, sdt = a.sqrt_dt, g4 = a.g4, beta = a.beta;
         const double inv_sdt = HC ? a.inv_sdt : 1.0 / sdt, inv_dt = HC ? a.inv_dt : 1.0 / dt;

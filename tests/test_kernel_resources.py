@@ -23,13 +23,14 @@ STEP = re.compile(r"k_stepILi(\d+)ELi(\d+)ELi(\d+)E([df])Lb([01])E")
 
 # (family, R, MODE, RT, DUAL) -> (max VGPR spills, max scratch bytes): the documented exceptions. The metric's two-slot
 # body (DUAL, MODE 2 and its MODE 1 variant) keeps 2 spilled registers outside the step loop (12 B per lane, written
-# once per wave); the IHO fp64 R = 16 kernel (N <= 1024, one wave per SIMD) and the HO fp32 R = 32 kernel (N <= 2048)
-# spill a few registers into AGPR-free VGPR lanes (no scratch)
+# once per wave); the IHO fp64 R = 16 kernel (N <= 1024, one wave per SIMD), the HO fp32 R = 32 kernels (N <= 2048) and
+# the fp32 IHO MODE 0 fallback spill a few registers, mostly into AGPRs (C5's own MODE 1 kernel: none)
 EXCEPTIONS = {
     (1, 8, 2, "d", 1): (2, 12),
     (1, 8, 1, "d", 1): (2, 12),
     (1, 16, 2, "d", 0): (8, 0),
     (1, 16, 1, "d", 0): (8, 0),
+    (1, 32, 0, "f", 0): (12, 0),   # the fp32 IHO MODE 0 fallback (tables from L2): spills into AGPR lanes, no scratch
     (0, 32, 2, "f", 0): (8, 28),
     (0, 32, 1, "f", 0): (8, 12),
     (0, 32, 0, "f", 0): (8, 0),

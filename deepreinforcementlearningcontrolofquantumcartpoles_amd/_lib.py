@@ -38,7 +38,7 @@ EXPORTS = (
     "qc_mactor_flat_len", "qc_mactor_load", "qc_mactor_act",
     "qc_replay_create", "qc_replay_destroy", "qc_replay_last_error", "qc_replay_set_stream", "qc_replay_store",
     "qc_replay_store_xp", "qc_replay_sample", "qc_replay_update", "qc_replay_rebuild", "qc_replay_stats",
-    "qc_replay_buffers", "qc_set_seed_mt19937_envs",
+    "qc_replay_buffers", "qc_set_seed_mt19937_envs", "qc_mt19937_normals",
     "qc_server_create", "qc_server_run", "qc_server_stop", "qc_server_stats", "qc_server_timing", "qc_server_last_error",
     "qc_server_destroy", "qc_env_tail",
 )
@@ -200,6 +200,7 @@ def lib() -> ctypes.CDLL:
     L.qc_env_counters.argtypes = [vp, vp, vp]
     L.qc_set_seed_mt19937.argtypes = [vp, vp]
     L.qc_set_seed_mt19937_envs.argtypes = [vp, vp, vp]
+    L.qc_mt19937_normals.argtypes = [vp, ctypes.c_int32, vp, vp, vp, vp]
     L.qc_env_tail.argtypes = [vp, P(QcEnvTailArgs)]
     L.qc_server_create.argtypes = [P(QcParams), ctypes.c_int, i32, ctypes.c_char_p, d, P(vp)]
     L.qc_server_run.argtypes = [vp, d]

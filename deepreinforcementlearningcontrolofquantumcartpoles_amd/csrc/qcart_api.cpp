@@ -24,6 +24,7 @@ constexpr int kMaxSlots = 64;
 // qc_step calls of at most this many physics steps on at most this many envs read their tables from L2 (MODE 0)
 constexpr int kShortCallSteps = 10;
 constexpr int64_t kShortCallBatch = 4096;
+constexpr int64_t kSpreadBatch = 1024;   // 4 envs per CU of MI355X's 256: one per SIMD
 std::mutex g_err_mu;
 std::string g_create_err;
 
@@ -65,7 +66,11 @@ struct qc_handle {
     uint32_t dual_img = 0;
     int32_t* d_order_mixed = nullptr;   // [kMaxSlots][wpb]
     int32_t *d_kf = nullptr, *d_kb = nullptr;
-    int32_t* d_bad = nullptr;     // raised by k_group on an out-of-range action (qc_take_errors)
+    // raised by k_group / the MODE 0 step kernel on an out-of-range action (qc_take_errors): one word of pinned,
+    // coherent host memory mapped into the device, so that reading it after a stream synchronisation is a host
+    // load (a 4-byte device-to-host copy cost a copy kernel and a second synchronisation per step-server tick)
+    int32_t* d_bad = nullptr;
+    volatile int32_t* h_bad = nullptr;
 };
 
 namespace {
@@ -115,7 +120,7 @@ void free_dev(qc_handle* h) {
                      &h->d_force};
     for (auto p : dp)
         if (*p) { (void)hipFree(*p); *p = nullptr; }
-    if (h->d_bad) { (void)hipFree(h->d_bad); h->d_bad = nullptr; }
+    if (h->h_bad) { (void)hipHostFree((void*)h->h_bad); h->h_bad = nullptr; h->d_bad = nullptr; }
     if (h->d_kf) { (void)hipFree(h->d_kf); h->d_kf = nullptr; }
     if (h->d_order) { (void)hipFree(h->d_order); h->d_order = nullptr; h->order_cap = 0; }
     if (h->d_order_mixed) { (void)hipFree(h->d_order_mixed); h->d_order_mixed = nullptr; }
@@ -403,8 +408,16 @@ int qc_create(const qc_params* p, int device, qc_handle** out) {
     {
         std::vector<uint64_t> zero((size_t)std::max<int64_t>(p->batch, 1), 0);
         rc = upload(h, &h->d_ctr, zero.data(), zero.size());
-        const int32_t z = 0;
-        if (!rc) rc = upload(h, &h->d_bad, &z, 1);
+        void* hb = nullptr;
+        if (!rc) rc = hip_check(h, hipHostMalloc(&hb, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
+                                "hipHostMalloc");
+        if (!rc) {
+            h->h_bad = (volatile int32_t*)hb;
+            *h->h_bad = 0;
+            void* dp = nullptr;
+            rc = hip_check(h, hipHostGetDevicePointer(&dp, hb, 0), "hipHostGetDevicePointer");
+            h->d_bad = (int32_t*)dp;
+        }
     }
     if (rc) {
         set_create_err(h->err);
@@ -502,6 +515,18 @@ int qc_set_seed_mt19937_envs(qc_handle* h, const uint32_t* seeds, const uint8_t*
     return QC_OK;
 }
 int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds) { return qc_set_seed_mt19937_envs(h, seeds, nullptr); }
+int qc_mt19937_normals(qc_handle* h, int32_t n_steps, const int32_t* env_steps, const double* pre,
+                       const uint8_t* has_pre, double* noise) {
+    if (!h) return QC_EINVAL;
+    if (n_steps < 0) return fail(h, QC_EINVAL, "n_steps must be >= 0");
+    if (h->noise_mode != QC_NOISE_MT19937 || !h->d_mt) return fail(h, QC_EINVAL, "no MT19937 state (qc_set_seed_mt19937 first)");
+    if (!noise && h->p.batch > 0 && n_steps > 0) return fail(h, QC_EINVAL, "noise is null");
+    if (!pre != !has_pre) return fail(h, QC_EINVAL, "pre and has_pre go together");
+    DeviceGuard g(h->device);
+    if (launch_mt_normals(h->d_mt, h->p.batch, n_steps, env_steps, noise, h->stream, pre, has_pre))
+        return fail(h, QC_EHIP, "MT19937 normals kernel launch failed");
+    return QC_OK;
+}
 int qc_noise_mode(const qc_handle* h) { return h ? h->noise_mode : QC_EINVAL; }
 int qc_mt19937_state(qc_handle* h, uint32_t* out, const uint32_t* in) {
     if (!h) return QC_EINVAL;
@@ -583,6 +608,12 @@ int qc_step(qc_handle* h, void* psi, const int32_t* actions, int32_t default_act
             a.lds_bytes = 0;
             a.lds_img = 0;
             a.lds_nz = 0;
+        }
+        // a short MODE 0 call on up to 4 envs per CU: one env per block (QCART_SPREAD=0 turns it off, A/B)
+        static const bool spread = !(std::getenv("QCART_SPREAD") && std::atoi(std::getenv("QCART_SPREAD")) == 0);
+        if (spread && a.tab_mode == 0 && n_steps <= kShortCallSteps && h->p.batch <= kSpreadBatch && h->wpb > 1) {
+            a.spread = 1;
+            a.n_blocks = (uint32_t)h->p.batch;
         }
     }
     // grid moment orders above the step kernel's fused epilogue: the observation kernel runs after the step
@@ -916,13 +947,9 @@ int qc_env_tail(qc_handle* h, const qc_env_tail_args* in) {
 int qc_take_errors(qc_handle* h) {
     if (!h) return QC_EINVAL;
     DeviceGuard g(h->device);
-    int32_t v = 0;
-    if (hipMemcpyAsync(&v, h->d_bad, sizeof(v), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-        hipStreamSynchronize(h->stream) != hipSuccess)
-        return fail(h, QC_EHIP, "reading the error word failed");
-    if (!v) return QC_OK;
-    const int32_t z = 0;
-    (void)hipMemcpy(h->d_bad, &z, sizeof(z), hipMemcpyHostToDevice);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(h, QC_EHIP, "reading the error word failed");
+    if (!*h->h_bad) return QC_OK;
+    *h->h_bad = 0;
     return fail(h, QC_EINVAL, "an action out of [0, n_slots) reached qc_step (clamped by the kernels)");
 }
 

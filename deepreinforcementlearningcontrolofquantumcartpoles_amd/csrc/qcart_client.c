@@ -31,6 +31,7 @@ struct qcc {
     double* psi;   /* this slot's state row [2N] */
     double* obs;   /* this slot's observation row [QCS_MAX_OBS] */
     int index;
+    double spin_s;   /* how long a call polls its done word before sleeping on the tick word */
     char err[160];
 };
 
@@ -93,6 +94,11 @@ int qcc_open(const char* name, qcc** out) {
     c->hdr = h;
     c->slot = &slots[idx];
     c->index = idx;
+    {
+        /* QCC_SPIN_US: a tick is tens of microseconds, a futex wake-up adds its own; the default polls for 150 us */
+        const char* v = getenv("QCC_SPIN_US");
+        c->spin_s = (v && *v ? atof(v) : 150.0) * 1e-6;
+    }
     c->psi = (double*)(m + h->psi_off) + (size_t)idx * 2 * (size_t)h->N;
     c->obs = (double*)(m + h->obs_off) + (size_t)idx * QCS_MAX_OBS;
     c->slot->pid = (int32_t)getpid();
@@ -155,11 +161,15 @@ static int call(qcc* c) {
         syscall(SYS_futex, &h->kick, FUTEX_WAKE, 1, NULL, NULL, 0);
     }
     /* a short spin (a tick takes tens of microseconds), then sleep on the tick word */
-    for (int i = 0; i < 2000; ++i) {
-        if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) return s->status;
-        __builtin_ia32_pause();
-    }
     const double t0 = now_s();
+    for (int i = 0;; ++i) {
+        if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) {
+            if (s->status) set_err(c, s->err);
+            return s->status;
+        }
+        __builtin_ia32_pause();
+        if ((i & 31) == 31 && now_s() - t0 > c->spin_s) break;
+    }
     for (;;) {
         __atomic_store_n(&s->waiting, 1u, __ATOMIC_SEQ_CST);
         const uint32_t t = __atomic_load_n(&h->tick, __ATOMIC_SEQ_CST);

@@ -40,23 +40,10 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
         const int s = actions ? actions[e] : default_action;
         return s < 0 ? 0 : (s >= n_slots ? n_slots - 1 : s);
     };
-    // the counts: per wave chunk of 64 envs, one LDS atomic per distinct slot of the chunk (a ballot per slot)
-    // instead of one per env — 1024 threads hammering 22 counters serialised on the LDS (0.1 ms at B = 65 536)
-    const int lane = t & 63;
-    const int64_t wstride = (int64_t)blockDim.x;
-    for (int64_t e0 = t - lane; e0 < B; e0 += wstride) {
-        const int64_t e = e0 + lane;
-        const bool valid = e < B;
-        const int s = valid ? slot_of(e) : -1;
-        if (valid && actions && s != kGroupSlots && (actions[e] < 0 || actions[e] >= n_slots)) bad[0] = 1;
-        uint64_t rem = __ballot(valid);
-        while (rem) {
-            const int leader = __ffsll((unsigned long long)rem) - 1;
-            const int sl = __builtin_amdgcn_readlane(s, leader);
-            const uint64_t m = __ballot(s == sl) & rem;
-            if (lane == leader) atomicAdd(&cnt[sl], __popcll(m));
-            rem &= ~m;
-        }
+    for (int64_t e = t; e < B; e += blockDim.x) {
+        const int s = slot_of(e);
+        if (actions && s != kGroupSlots && (actions[e] < 0 || actions[e] >= n_slots)) bad[0] = 1;
+        atomicAdd(&cnt[s], 1);
     }
     __syncthreads();
     if (t == 0) {
@@ -102,26 +89,11 @@ __global__ __launch_bounds__(1024) void k_group(const int32_t* __restrict__ acti
         if (s2 >= 0 && head_mix[s2] >= 0 && G == start[s2] / g) return order_mixed + head_mix[s2] * g + p % g;
         return order + (G - nmix_le[s]) * g + p % g;
     };
-    for (int64_t e0 = t - lane; e0 < B; e0 += wstride) {
-        const int64_t e = e0 + lane;
-        const bool valid = e < B;
-        const int s = valid ? slot_of(e) : -1;
-        uint64_t rem = __ballot(valid);
-        int k = 0;
-        while (rem) {   // one reservation per distinct slot of the chunk; lanes take consecutive places
-            const int leader = __ffsll((unsigned long long)rem) - 1;
-            const int sl = __builtin_amdgcn_readlane(s, leader);
-            const uint64_t m = __ballot(s == sl) & rem;
-            int k0 = 0;
-            if (lane == leader) k0 = atomicAdd(&cur[sl], __popcll(m));
-            k0 = __builtin_amdgcn_readlane(k0, leader);
-            if (s == sl) k = k0 + __popcll(m & ((1ull << lane) - 1ull));
-            rem &= ~m;
-        }
-        if (valid) {
-            if (start[s] >= 0) *packed_dst(s, start[s] + k) = (int32_t)e;
-            else order[off[s] + k] = (int32_t)e;
-        }
+    for (int64_t e = t; e < B; e += blockDim.x) {
+        const int s = slot_of(e);
+        const int k = atomicAdd(&cur[s], 1);
+        if (start[s] >= 0) *packed_dst(s, start[s] + k) = (int32_t)e;
+        else order[off[s] + k] = (int32_t)e;
     }
     if (t < kBuckets && start[t] < 0)
         for (int p = cnt[t]; p < (cnt[t] + g - 1) / g * g; ++p) order[off[t] + p] = -1;

@@ -126,6 +126,7 @@ struct KArgs {
     double inv_sdt, inv_dt, k_hisdt, k_qisdt, k_hidt, k_qidt, k_qdt, k_qsdt, k_dz, k_sb, b2, b3, b4;
     double x2h;                // IHO: -1/omega, X^2's +-2 bands as a multiple of H's (k_step X2H)
     int32_t* bad;              // the handle's error word: an out-of-range action of an ungrouped call (MODE 0)
+    int32_t spread;            // MODE 0 without order: one env per block (wave 0; the block's other waves idle)
 };
 
 // measurement-record update (qcart_record.hip, qc_record)
@@ -177,7 +178,7 @@ int launch_env_tail(const EnvTailArgs& a, void* stream);
 constexpr int kMtWords = 626;
 int launch_mt_seed(const uint32_t* seeds, const uint8_t* mask, int64_t B, uint32_t* st, void* stream);
 int launch_mt_normals(uint32_t* st, int64_t B, int32_t n_steps, const int32_t* env_steps, double* noise,
-                      void* stream);
+                      void* stream, const double* pre = nullptr, const uint8_t* has_pre = nullptr);
 int launch_fill_u64(uint64_t* p, int64_t n, uint64_t v, void* stream);
 
 // host-side launchers (qcart_kernels.hip)

@@ -1239,7 +1239,7 @@ __device__ __forceinline__ decltype(auto) step_kargs(const KArgs& a) {
 // MODE 3: a two-slot block (k_group's remainder workgroups, KArgs::order_mixed): MODE 1 reads (tables in
 // LDS, scan composites from the slot's global block) with both slots' images in LDS, a.lds_img bytes apart;
 // every wave uses its own env's slot and image
-template <int FAM, int R, int MODE, typename RT>
+template <int FAM, int R, int MODE, typename RT, bool SKIP>
 __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, const uint32_t blk) {
     QC_KSTAMP_ENTRY();
     constexpr int KL = Fam<FAM>::KL;
@@ -1256,13 +1256,16 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     constexpr bool T2 = (MODE == 1 || MODE == 2 || MODE == 4) && IMG_END > 131072u;
     const int lane = threadIdx.x & 63;
     const int gl = lane;   // lane of the env
-    // env of this wave: order (envs grouped by force slot, EPB per block, -1 = idle) or identity
-    const int64_t e0 = order ? (int64_t)order[blk * EPB] : (int64_t)blk * EPB;
+    // env of this wave: order (envs grouped by force slot, EPB per block, -1 = idle) or identity; a spread MODE 0
+    // launch (short calls on small batches, latency-bound) runs one env per block, so that every env has a SIMD
+    // (and a CU's L1) to itself instead of sharing one with up to seven others
+    const bool spr = MODE == 0 && a.spread;
+    const int64_t e0 = order ? (int64_t)order[blk * EPB] : (spr ? (int64_t)blk : (int64_t)blk * EPB);
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
     // (wave-uniform: made explicit, so every env-derived address lives in SGPRs)
     const int ei = (int)(threadIdx.x >> 6);
     const int64_t env = (int64_t)__builtin_amdgcn_readfirstlane(
-        order ? order[blk * EPB + ei] : (int)(blk * EPB + ei));
+        order ? order[blk * EPB + ei] : (spr ? (ei == 0 ? (int)blk : -1) : (int)(blk * EPB + ei)));
     const bool active = env >= 0 && env < a.B;
     auto clamp_slot = [&](int s) { return s < 0 ? 0 : (s >= a.n_slots ? a.n_slots - 1 : s); };
     // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
@@ -1379,8 +1382,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     };
     // a frozen env (no step budget: the not-finished envs of a reset interval) with no observation or
     // termination index requested is only reported (fail_step 0): its psi is neither read nor written (fp64
-    // kernels; the fp32 R = 32 kernels sit at their register limit, where the extra exit moved their spills)
-    constexpr bool FROZEN_SKIP = sizeof(RT) == 8;
+    // single-body kernels; the fp32 R = 32 kernels sit at their register limit, where the extra exit moved their
+    // spills, and in the two-slot DUAL kernel the exit cost 11 more SGPR spill lanes and 3% of the metric launch:
+    // 23.8 vs 23.1 ms in one call)
+    constexpr bool FROZEN_SKIP = SKIP && sizeof(RT) == 8;
     if (FROZEN_SKIP && !a.obs_out && !a.term_step && steps_of() == 0) {
         if (lane == 0 && a.fail_step) a.fail_step[env] = 0;
         return;
@@ -2090,14 +2095,14 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
     if constexpr (DUAL) {
         const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(*a.n_mixed_used);
         if (blockIdx.x < m) {
-            step_body<FAM, R, 3, RT>(a, a.order_mixed, blockIdx.x);
+            step_body<FAM, R, 3, RT, false>(a, a.order_mixed, blockIdx.x);
             return;
         }
         // the grid has n_mixed - m more blocks than a.order holds
         if (blockIdx.x - m >= a.n_blocks) return;
-        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x - m);
+        step_body<FAM, R, MODE, RT, false>(a, a.order, blockIdx.x - m);
     } else {
-        step_body<FAM, R, MODE, RT>(a, a.order, blockIdx.x);
+        step_body<FAM, R, MODE, RT, true>(a, a.order, blockIdx.x);
     }
 }
 

@@ -93,9 +93,11 @@ __device__ __forceinline__ void twist(uint32_t* mt, int lane) {
 
 // One wave per env: the env's min(n_steps, env_steps[e]) steps need 4 words each; normals go to
 // noise[k][e][0..1] (the step kernel's injected-noise layout). Steps past the env's budget are left
-// untouched (the step kernel never reads them).
+// untouched (the step kernel never reads them). With `pre` (optional, [B][2]) an env with has_pre[e] != 0 already
+// drew its first step's pair into pre[e] (the step server's prefetch): that pair becomes step 0 and only the
+// remaining steps draw from the stream.
 __global__ __launch_bounds__(256) void k_mt_normals(uint32_t* st, int64_t B, int32_t n_steps, const int32_t* env_steps,
-                                                    double* noise) {
+                                                    double* noise, const double* pre, const uint8_t* has_pre) {
     __shared__ uint32_t lds[4][kN + 1];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e = (int64_t)blockIdx.x * 4 + w;
@@ -106,13 +108,18 @@ __global__ __launch_bounds__(256) void k_mt_normals(uint32_t* st, int64_t B, int
         n_my = b < 0 ? 0 : (b < n_my ? b : n_my);
     }
     if (n_my <= 0) return;
+    const int s0 = (pre && has_pre[e]) ? 1 : 0;
+    if (s0) {
+        if (lane < 2) noise[(size_t)e * 2 + lane] = pre[(size_t)e * 2 + lane];
+        if (n_my == 1) return;
+    }
     uint32_t* mt = lds[w];
     uint32_t* g = st + (size_t)e * kMtWords;
     for (int i = lane; i < kN; i += 64) mt[i] = g[i];
     int idx = (int)g[kN];   // even: words are only ever consumed in pairs
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const int64_t need = 4 * (int64_t)n_my;
+    const int64_t need = 4 * (int64_t)(n_my - s0);
     int64_t done = 0;
     while (done < need) {
         if (idx >= kN) {
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256) void k_mt_normals(uint32_t* st, int64_t B, int
             // a zero first word: MKL returns the finite radius kMklZeroWordRadius, not inf (pinned, below)
             const double rad = w1 ? sqrt(-2.0 * log(u1)) : kMklZeroWordRadius;
             const double x = rad * sin(6.283185307179586 * u2);
-            const int64_t n = done / 2 + p;   // normal index of the env: step n / 2, component n % 2
+            const int64_t n = done / 2 + p + 2 * s0;   // normal index of the env: step n / 2, component n % 2
             noise[((size_t)(n >> 1) * B + e) * 2 + (n & 1)] = x;
         }
         idx += avail;
@@ -153,10 +160,10 @@ int launch_mt_seed(const uint32_t* seeds, const uint8_t* mask, int64_t B, uint32
 }
 
 int launch_mt_normals(uint32_t* st, int64_t B, int32_t n_steps, const int32_t* env_steps, double* noise,
-                      void* stream) {
+                      void* stream, const double* pre, const uint8_t* has_pre) {
     if (B <= 0 || n_steps <= 0) return 0;
     hipLaunchKernelGGL(k_mt_normals, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, st, B, n_steps,
-                       env_steps, noise);
+                       env_steps, noise, pre, has_pre);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

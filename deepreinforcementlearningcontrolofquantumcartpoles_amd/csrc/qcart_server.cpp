@@ -21,6 +21,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -63,6 +64,10 @@ struct qc_server {
     std::string name, err;
     qc_handle* h = nullptr;
     hipStream_t stream = nullptr;
+    // the tick's completion: an event polled by this (already busy) server thread — hipStreamSynchronize's
+    // blocking wait adds its wake-up latency to every tick; QCART_SERVER_SYNC=block restores it (A/B)
+    hipEvent_t done = nullptr;
+    bool spin_sync = true;
     // shared memory
     int fd = -1;
     size_t shm_bytes = 0;
@@ -83,6 +88,22 @@ struct qc_server {
     int32_t *fs1 = nullptr, *d_fs1 = nullptr, *fb10 = nullptr, *d_fb10 = nullptr; // [P]
     double *xe = nullptr, *d_xe = nullptr;           // [P]
     double *obs = nullptr, *d_obs = nullptr;         // [P][n_obs]
+    // the clients' state rows registered with HIP (device-mapped): the kernels step them in place, no copy in or out
+    // (QCART_SERVER_INPLACE=0, or a failed registration: copies through `psi`)
+    double* d_spsi = nullptr;
+    bool inplace = false;
+    // MT19937 prefetch (QCART_SERVER_PREFETCH=0 turns it off): after a tick, every owned env that has no drawn pair
+    // draws its next step's pair into d_pre (has_pre = 1) while the clients turn round; a 1-step call then steps on
+    // it directly and a 10-step call takes it as its step 0 — the normals kernel leaves the tick's critical path.
+    // The streams advance exactly as without it (the same words in the same order).
+    bool prefetch = true;
+    double* d_pre = nullptr;                         // device [P][2]
+    double* d_n10 = nullptr;                         // device [10][P][2]
+    std::vector<uint8_t> pre_ok;                     // [P] env e has a drawn pair in d_pre (host bookkeeping)
+    uint8_t *has_pre = nullptr, *d_has_pre = nullptr;   // [P] pre_ok as the 10-step draw reads it (written before
+                                                        // the launch: a kernel reads mapped memory when it runs)
+    int32_t *gen = nullptr, *d_gen = nullptr;        // [P] draw budgets of the tick's 1-step envs without a pair
+    int32_t *pf = nullptr, *d_pf = nullptr;          // [P] draw budgets of the prefetch
     std::vector<uint32_t> served;                    // last served req per slot
     std::map<double, int> custom;                    // off-grid force -> slot
     double cur_dt = 0, cur_gamma = 0;
@@ -123,9 +144,13 @@ int slot_of(qc_server* s, double force, int& slot) {
 void free_server(qc_server* s) {
     if (s->h) qc_destroy(s->h);
     void* hb[] = {s->psi, s->act, s->st1, s->st10, s->seeds, s->mask, s->q1, s->xm1, s->q10, s->xm10, s->fs1, s->fb10,
-                  s->xe, s->obs};
+                  s->xe, s->obs, s->has_pre, s->gen, s->pf};
     for (void* b : hb)
         if (b) (void)hipHostFree(b);
+    if (s->d_pre) (void)hipFree(s->d_pre);
+    if (s->d_n10) (void)hipFree(s->d_n10);
+    if (s->inplace && s->shm) (void)hipHostUnregister(s->shm + s->hdr->psi_off);
+    if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->shm) {
         if (s->hdr) __atomic_store_n(&s->hdr->alive, 0u, __ATOMIC_SEQ_CST);
@@ -152,10 +177,11 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         if (r.op == QCS_OP_SET_SEED) {
             s->seeds[e] = r.seed;
             s->mask[e] = 1;
+            s->pre_ok[e] = 0;   // a drawn pair belongs to the old stream
             any_seed = true;
             continue;
         }
-        std::memcpy(s->psi + (size_t)e * 2 * N, s->spsi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
+        if (!s->inplace) std::memcpy(s->psi + (size_t)e * 2 * N, s->spsi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
         if (r.op == QCS_OP_STEP) (r.n == 10 ? g10 : g1).push_back(e);
         else if (r.op == QCS_OP_X_EXPECT) any_x = true;
         else any_obs = true;
@@ -203,24 +229,50 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
             }
             if (ok.empty()) continue;
             const int n = grp == 0 ? 1 : 10;
-            rc = qc_step(s->h, s->d_psi, s->d_act, s->p.n_actions / 2, n, grp == 0 ? s->d_st1 : s->d_st10, nullptr,
-                         grp == 0 ? s->d_q1 : s->d_q10, grp == 0 ? s->d_xm1 : s->d_xm10, grp == 0 ? s->d_fs1 : nullptr,
-                         nullptr, nullptr);
+            const double* noise = nullptr;   // nullptr: qc_step draws from the streams itself
+            if (s->prefetch) {
+                if (grp == 0) {
+                    // the pairs of the group's envs that have none yet (after a reseed or a 10-step call)
+                    bool any = false;
+                    for (int e = 0; e < P; ++e) s->gen[e] = 0;
+                    for (int e : ok)
+                        if (!s->pre_ok[e]) { s->gen[e] = 1; any = true; }
+                    if (any) rc = qc_mt19937_normals(s->h, 1, s->d_gen, nullptr, nullptr, s->d_pre);
+                    noise = s->d_pre;
+                } else {
+                    for (int e = 0; e < P; ++e) s->has_pre[e] = s->pre_ok[e];
+                    rc = qc_mt19937_normals(s->h, 10, s->d_st10, s->d_pre, s->d_has_pre, s->d_n10);
+                    noise = s->d_n10;
+                }
+                if (rc) { err_all(ok, rc); continue; }
+            }
+            rc = qc_step(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_act, s->p.n_actions / 2, n,
+                         grp == 0 ? s->d_st1 : s->d_st10, noise, grp == 0 ? s->d_q1 : s->d_q10,
+                         grp == 0 ? s->d_xm1 : s->d_xm10, grp == 0 ? s->d_fs1 : nullptr, nullptr, nullptr);
+            // the pairs consumed (a 10-step draw took them already)
+            if (s->prefetch && (grp == 1 || rc == QC_OK))
+                for (int e : ok) s->pre_ok[e] = 0;
             // simulate_10_steps' Fail is the boundary test of the final state (IHO/simulation_i.cpp:391-421)
-            if (rc == QC_OK && grp == 1) rc = qc_boundary_fail(s->h, s->d_psi, s->d_fb10);
+            if (rc == QC_OK && grp == 1) rc = qc_boundary_fail(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_fb10);
             if (rc) err_all(ok, rc);
         }
     }
     if (any_x) {
-        const int rc = qc_x_expectation(s->h, s->d_psi, s->d_xe);
+        const int rc = qc_x_expectation(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_xe);
         if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op == QCS_OP_X_EXPECT) es.push_back(e); err_all(es, rc); }
     }
     if (any_obs) {
-        const int rc = qc_moments(s->h, s->d_psi, s->d_obs);
+        const int rc = qc_moments(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_obs);
         if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op >= QCS_OP_MOMENTS) es.push_back(e); err_all(es, rc); }
     }
     const double t_l = now_us();
-    if (hipStreamSynchronize(s->stream) != hipSuccess) {
+    hipError_t e = hipSuccess;
+    if (s->spin_sync && hipEventRecord(s->done, s->stream) == hipSuccess) {
+        while ((e = hipEventQuery(s->done)) == hipErrorNotReady) cpu_relax();
+    } else {
+        e = hipStreamSynchronize(s->stream);
+    }
+    if (e != hipSuccess) {
         qc_sync(s->h);
         err_all(pend, QC_EHIP);
     }
@@ -233,7 +285,7 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         const Req& r = rq[e];
         if (sl.status == QC_OK) {
             if (r.op == QCS_OP_STEP) {
-                std::memcpy(s->spsi + (size_t)e * 2 * N, s->psi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
+                if (!s->inplace) std::memcpy(s->spsi + (size_t)e * 2 * N, s->psi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
                 if (r.n == 10) {
                     sl.q = s->q10[(size_t)9 * P + e];
                     sl.xmean = s->xm10[(size_t)9 * P + e];
@@ -254,6 +306,19 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         __atomic_store_n(&sl.done, s->served[e], __ATOMIC_SEQ_CST);
     }
     s->t_publish += now_us() - t_g;
+    if (s->prefetch) {
+        // every owned env without a drawn pair draws its next one now, while the clients turn round (the next tick's
+        // launches queue behind it on the stream; pf is rewritten only after the next tick's completion)
+        bool any = false;
+        for (int e = 0; e < P; ++e) {
+            s->pf[e] = 0;
+            if (ld_acq(&s->slots[e].owner) && !s->pre_ok[e]) { s->pf[e] = 1; s->pre_ok[e] = 1; any = true; }
+        }
+        if (any && qc_mt19937_normals(s->h, 1, s->d_pf, nullptr, nullptr, s->d_pre) != QC_OK) {
+            for (int e = 0; e < P; ++e) if (s->pf[e]) s->pre_ok[e] = 0;
+            s->prefetch = false;   // (a launch failure: draw in qc_step from now on)
+        }
+    }
     s->ticks++;
     s->calls += (int64_t)pend.size();
     s->hdr->ticks = (uint64_t)s->ticks;
@@ -300,14 +365,28 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     auto bail = [&](int code, const std::string& m) { s->err = m; free_server(s); delete s; return code; };
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(QC_EHIP, "hipStreamCreate failed");
+    if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess)
+        return bail(QC_EHIP, "hipEventCreate failed");
+    {
+        const char* m = std::getenv("QCART_SERVER_SYNC");
+        s->spin_sync = !(m && std::strcmp(m, "block") == 0);
+    }
     qc_set_stream(s->h, s->stream);
     if (host_alloc(&s->psi, &s->d_psi, (size_t)P * 2 * N) || host_alloc(&s->act, &s->d_act, P) ||
         host_alloc(&s->st1, &s->d_st1, P) || host_alloc(&s->st10, &s->d_st10, P) || host_alloc(&s->seeds, &s->d_seeds, P) ||
         host_alloc(&s->mask, &s->d_mask, P) || host_alloc(&s->q1, &s->d_q1, P) || host_alloc(&s->xm1, &s->d_xm1, P) ||
         host_alloc(&s->q10, &s->d_q10, (size_t)10 * P) || host_alloc(&s->xm10, &s->d_xm10, (size_t)10 * P) ||
         host_alloc(&s->fs1, &s->d_fs1, P) || host_alloc(&s->fb10, &s->d_fb10, P) || host_alloc(&s->xe, &s->d_xe, P) ||
-        host_alloc(&s->obs, &s->d_obs, (size_t)P * (s->n_obs > 0 ? s->n_obs : 1)))
+        host_alloc(&s->obs, &s->d_obs, (size_t)P * (s->n_obs > 0 ? s->n_obs : 1)) ||
+        host_alloc(&s->has_pre, &s->d_has_pre, P) || host_alloc(&s->gen, &s->d_gen, P) || host_alloc(&s->pf, &s->d_pf, P))
         return bail(QC_ENOMEM, "pinned host buffers");
+    {
+        const char* m = std::getenv("QCART_SERVER_PREFETCH");
+        s->prefetch = !(m && std::atoi(m) == 0);
+    }
+    if (hipMalloc((void**)&s->d_pre, sizeof(double) * 2 * P) != hipSuccess ||
+        hipMalloc((void**)&s->d_n10, sizeof(double) * 20 * P) != hipSuccess)
+        return bail(QC_ENOMEM, "device noise buffers");
     // every env starts on seed 0's MT19937 stream (the plain drop-in's state before the first set_seed)
     rc = qc_set_seed_mt19937(s->h, s->d_seeds);
     if (rc == QC_OK) rc = qc_sync(s->h);
@@ -330,6 +409,24 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     s->slots = (qcs_slot*)(s->shm + slot_off);
     s->spsi = (double*)(s->shm + psi_off);
     s->sobs = (double*)(s->shm + obs_off);
+    {
+        // the state rows (page-aligned, whole pages) registered and device-mapped: stepped in place
+        // in place needs the short-call step kernel (qc_step's MODE 0 for n <= 10 on a batch <= 4096), which leaves a
+        // frozen env's row unread and unwritten: the rows of clients not in the tick are theirs to write meanwhile
+        const char* m = std::getenv("QCART_SERVER_INPLACE");
+        const char* m0 = std::getenv("QCART_SHORT_MODE0");
+        if (!(m && std::atoi(m) == 0) && !(m0 && std::atoi(m0) == 0) && P <= 4096 &&
+            hipHostRegister(s->shm + psi_off, obs_off - psi_off, hipHostRegisterMapped) == hipSuccess) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, s->shm + psi_off, 0) == hipSuccess) {
+                s->d_spsi = (double*)d;
+                s->inplace = true;
+            } else {
+                (void)hipHostUnregister(s->shm + psi_off);
+            }
+        }
+        (void)hipGetLastError();
+    }
     qcs_header* H = s->hdr;
     H->magic = QCS_MAGIC;
     H->version = QCS_VERSION;
@@ -351,6 +448,7 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     H->f_max = p->f_max;
     H->n_actions = p->n_actions;
     s->served.assign(P, 0u);
+    s->pre_ok.assign(P, 0);
     __atomic_store_n(&H->alive, 1u, __ATOMIC_SEQ_CST);
     *out = s;
     return QC_OK;

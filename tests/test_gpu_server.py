@@ -133,6 +133,54 @@ def test_concurrent_clients_equal_the_plain_dropin():
     assert stats["ticks"] < stats["calls"]            # ticks served several envs at once
 
 
+def _mixed_calls(m, c, n_max, dt, gamma):
+    """One client's mixed sequence: step calls, simulate_10_steps every 7th call, a reseed half way — the step
+    server's MT19937 prefetch (a drawn pair per env, consumed by a step, taken as step 0 of a 10-step call, dropped
+    by a reseed) must leave every stream exactly where the plain drop-in's is."""
+    m.set_seed(300 + c)
+    st = np.zeros(n_max + 1, np.complex128)
+    st[0] = 1.0
+    out = []
+    for k in range(120):
+        F = 0.8 * ((k // 40 + c) % 3 - 1)
+        if k == 61:
+            m.set_seed(400 + c)
+        if k % 7 == 3:
+            out.append(tuple(m.simulate_10_steps(st, dt, F, gamma)))
+        else:
+            out.append(tuple(m.step(st, dt, F, gamma)))
+    return st.copy(), out
+
+
+def test_served_mixed_calls_keep_the_streams_of_the_plain_dropin():
+    """Three clients with mixed 1-step / 10-step calls and a reseed (the server's prefetched pairs in every
+    state): states and returns bitwise equal to the plain drop-in's."""
+    n_max, P = 127, 3
+    dt, gamma = 1 / 1440, 2 * pi
+    plain = S.load(cfg.IHO, n_max=n_max)
+    want = [_mixed_calls(plain, c, n_max, dt, gamma) for c in range(P)]
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=P, name=name, n_max=n_max).start()
+    got = [None] * P
+    errs = []
+
+    def run(c):
+        try:
+            m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max), name)
+            got[c] = _mixed_calls(m, c, n_max, dt, gamma)
+            m.close()
+        except Exception as e:   # reported below
+            errs.append(repr(e))
+    ts = [threading.Thread(target=run, args=(c,)) for c in range(P)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    srv.close()
+    assert not errs, errs
+    for c in range(P):
+        assert np.array_equal(got[c][0], want[c][0]), c
+        assert got[c][1] == want[c][1], c
+
+
 def test_served_errors():
     """A module whose parameters differ from the server's is refused at load (the drivers' check_settings
     handshake); a full server refuses one more client; a stopped server fails a waiting call."""

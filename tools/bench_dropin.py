@@ -115,6 +115,15 @@ def serve(args):
     srv.close()
 
 
+def cpu_stat():
+    """The cgroup's CPU-quota throttling counters (cgroup v2 cpu.stat; {} where absent): P spinning processes over
+    a CPU quota stall together for the rest of the quota period."""
+    try:
+        return {k: int(v) for k, v in (l.split() for l in open("/sys/fs/cgroup/cpu.stat"))}
+    except (OSError, ValueError):
+        return {}
+
+
 def fan_out(args, kind, P):
     go = os.path.join(tempfile.mkdtemp(prefix="qcart_dropin_"), "go")
     env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
@@ -148,6 +157,7 @@ def fan_out(args, kind, P):
         if not p.stdout.readline().startswith("ready"):
             p.wait()
             fail(r)
+    cs0 = cpu_stat()
     open(go, "w").close()
     res = []
     for r, p in enumerate(procs):
@@ -155,6 +165,7 @@ def fan_out(args, kind, P):
         if p.returncode != 0:
             fail(r)
         res.append(json.loads(out.strip().splitlines()[-1]))
+    cs1 = cpu_stat()
     srv_stats = None
     if server is not None:
         out, _ = server.communicate(input="", timeout=120)
@@ -172,6 +183,9 @@ def fan_out(args, kind, P):
     agg = inside / (T1 - T0)
     row = {"kind": kind, "procs": P, "step_calls_per_s": agg, "per_proc_calls_per_s": agg / P,
            "us_per_call": P / agg * 1e6, "seconds": args.seconds, "common_window_s": T1 - T0}
+    if cs0 and cs1:
+        row["cgroup"] = {k: cs1[k] - cs0.get(k, 0) for k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")
+                         if k in cs1}
     if srv_stats:
         row["server"] = dict(srv_stats, calls_per_tick=srv_stats["calls"] / max(1, srv_stats["ticks"]))
     return row

@@ -131,10 +131,12 @@ def fan_out(args, kind, P):
     name = f"/qcart_bench_{os.getpid()}_{P}"
     if kind == "server":
         serr = open(go + ".server_err", "w+")
-        server = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--serve", "--name", name,
-                                   "--max-clients", str(P), "--n-max", str(args.n_max),
-                                   "--batch-wait-us", str(args.batch_wait_us)],
-                                  cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=serr,
+        cmd = [sys.executable, os.path.abspath(__file__), "--serve", "--name", name, "--max-clients", str(P),
+               "--n-max", str(args.n_max), "--batch-wait-us", str(args.batch_wait_us)]
+        if args.server_prof:   # the server under rocprofv3 (kernel + HIP API trace: tools/server_timeline.py)
+            cmd = ["rocprofv3", "--kernel-trace", "--hip-trace", "--output-format", "csv", "-d",
+                   os.path.abspath(args.server_prof), "-o", "run", "--"] + cmd
+        server = subprocess.Popen(cmd, cwd=ROOT, env=dict(env, TMPDIR="/tmp") if args.server_prof else env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=serr,
                                   text=True)
         if not server.stdout.readline().startswith("ready"):
             server.wait()
@@ -207,6 +209,7 @@ def main():
     ap.add_argument("--name", default="")
     ap.add_argument("--max-clients", type=int, default=16)
     ap.add_argument("--batch-wait-us", type=float, default=40.0)
+    ap.add_argument("--server-prof", default="", help="run the server under rocprofv3 kernel + HIP trace into DIR")
     args = ap.parse_args()
     if args.serve:
         return serve(args)

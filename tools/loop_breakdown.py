@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     for p in ("void ", "qcart::"):
         n = n.replace(p, "")
     if "at::native" in n or "at::" in n:
@@ -30,13 +30,14 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--input", default="xp")
+    ap.add_argument("--reset", default="immediate", choices=("immediate", "deferred"))
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out", "loop_bd"))
     a = ap.parse_args()
     env = dict(os.environ, TMPDIR="/tmp")
     cmd = ["rocprofv3", "--kernel-trace", "--marker-trace", "--output-format", "csv", "-d", a.dir, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "tools", "bench_loop.py"), "--batch", str(a.batch), "--steps",
-           str(a.steps), "--input", a.input, "--marker"]
+           str(a.steps), "--input", a.input, "--reset", a.reset, "--marker"]
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=900)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not line:
@@ -73,7 +74,7 @@ def main():
     if cur_e is not None:
         busy += (cur_e - cur_s) / 1e6
     wall = (t1 - t0) / 1e6
-    lines = [f"# tools/loop_breakdown.py: bench_loop --batch {a.batch} --steps {K} --input {a.input} under rocprofv3 "
+    lines = [f"# tools/loop_breakdown.py: bench_loop --batch {a.batch} --steps {K} --input {a.input} --reset {a.reset} under rocprofv3 "
              f"(kernel + marker trace), the 'timed' range only",
              f"# bench_loop: {res['ms_per_control_step']:.2f} ms per control step (its own clock, profiled run), "
              f"done fraction per control step {res.get('done_fraction_per_control_step', float('nan')):.4f}",

@@ -1267,6 +1267,26 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     const int64_t env = (int64_t)__builtin_amdgcn_readfirstlane(
         order ? order[blk * EPB + ei] : (spr ? (ei == 0 ? (int)blk : -1) : (int)(blk * EPB + ei)));
     const bool active = env >= 0 && env < a.B;
+    // MODE 0 (short calls: the drop-in, the step server's ticks): the env's state rows and step budget are requested
+    // here, beside its action, so that the three reads overlap — in a server tick all three live in host memory,
+    // and issued where they are used (action -> slot -> budget -> skip test -> rows) they were three PCIe round trips
+    // in a row: 17.0 vs 12.1 us per 16-env one-step kernel with everything in device memory
+    // (tools/short_call_probe.py). Rows early only where the registers are there (R <= 8 fp64 / 16 fp32: the
+    // IHO N = 1024 and grid N = 1025 fallbacks spilled 4 registers each with them)
+    constexpr bool PRE = MODE == 0 && R * sizeof(RT) <= 64;
+    cx<RT> psi[R];
+    int budget0 = 0;
+    if constexpr (MODE == 0) {
+        if (active) {
+            budget0 = a.env_steps ? a.env_steps[env] : a.n_steps;
+            if constexpr (PRE) {
+                const RT* g0 = (const RT*)a.psi + (size_t)env * a.N * 2;
+#pragma unroll
+                for (int j = 0; j < R; ++j)
+                    psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
+            }
+        }
+    }
     auto clamp_slot = [&](int s) { return s < 0 ? 0 : (s >= a.n_slots ? a.n_slots - 1 : s); };
     // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
     // a block shares its first env's slot)
@@ -1374,7 +1394,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's steps this call: min(n_steps, its budget)
     auto steps_of = [&]() {
         int n = a.n_steps;
-        if (a.env_steps) {
+        if (MODE == 0) {
+            n = budget0 < 0 ? 0 : (budget0 < n ? budget0 : n);
+        } else if (a.env_steps) {
             const int e = a.env_steps[env];
             n = e < 0 ? 0 : (e < n ? e : n);
         }
@@ -1397,14 +1419,15 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     load_coef<FAM, R>(cf, a, base);
 
     RT* gpsi = (RT*)a.psi + (size_t)env * N * 2;
-    cx<RT> psi[R];
     // psi: one whole-complex (16 B fp64 / 8 B fp32) access per row and lane; a wave's R accesses of a row index
     // cover its env's lines completely, so the L2 hands HBM whole lines. (Non-temporal 8-B accesses of the real
     // and imaginary halves, round 3's first variant, reached HBM as partial writes: 2.2 GB written per metric
     // launch for 0.54 GB of psi, 4.7 GB at C5, and 1.8x the read bytes)
+    if constexpr (!PRE) {
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-        psi[j] = (base + j < N) ? ld_cx<RT>(gpsi + 2 * (base + j)) : C(RT(0), RT(0));
+        for (int j = 0; j < R; ++j)
+            psi[j] = (base + j < N) ? ld_cx<RT>(gpsi + 2 * (base + j)) : C(RT(0), RT(0));
+    }
 
     const bool win_on = a.win_hi > a.win_lo;
     // X psi carried across steps (Fock families; on the grid X is diagonal and recomputed per row)

@@ -447,6 +447,47 @@ def test_table_placements_bitwise_equal(monkeypatch, case):
     assert torch.equal(y[0], outs[0][5])
 
 
+@pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513", "qo1025"])
+def test_short_call_layouts_bitwise_equal(case):
+    """Short calls (n <= 10 steps, tables from L2): a small batch runs one env per workgroup ("spread", batch <=
+    1024), a larger one eight envs per workgroup, and the state rows, budget and action are read together up front
+    (R <= 8). The same 37 envs stepped ten one-step calls in a 37-env handle and inside an 1100-env handle (the
+    other envs without a step budget) give bit-identical states, q and x_mean."""
+    ph = CASES[case]
+    B1, B2, K = 37, 1100, 10
+    rng = np.random.default_rng(3)
+    acts = torch.from_numpy(rng.integers(0, 21, B1).astype(np.int32)).cuda()
+    noise = torch.from_numpy(rng.standard_normal((K, 1, B1, 2))).cuda()
+    res = []
+    for B in (B1, B2):
+        st = Stepper(ph, B, 0, seed=11)
+        a = st.new_state()
+        if ph.fock:
+            st.reset(a, 1, arg0=16)
+        else:
+            st.reset(a, 2, arg0=0.0, arg1=0.0, arg2=1.0)
+        x = a[:B1].clone() if B == B1 else a
+        if B == B2:
+            x[:B1] = res[0][2]                                   # the same initial states
+        act = acts if B == B1 else torch.cat([acts, torch.full((B2 - B1,), 10, dtype=torch.int32, device="cuda")])
+        bud = torch.zeros(B, dtype=torch.int32, device="cuda")
+        bud[:B1] = 1
+        qs = []
+        for k in range(K):
+            nz = noise[k] if B == B1 else torch.cat([noise[k], torch.zeros((1, B2 - B1, 2), dtype=torch.float64,
+                                                                              device="cuda")], 1)
+            out = st.step(x, act, 1, noise=nz, env_steps=bud, want_q=True)
+            qs.append((out["q"][0, :B1].clone(), out["x_mean"][0, :B1].clone()))
+        torch.cuda.synchronize()
+        if B == B1:
+            res.append((x.clone(), qs, a[:B1].clone()))
+        else:
+            res.append((x[:B1].clone(), qs))
+    assert torch.equal(res[0][0], res[1][0])
+    for (q1, m1), (q2, m2) in zip(res[0][1], res[1][1]):
+        assert torch.equal(q1, q2) and torch.equal(m1, m2)
+
+
 @pytest.mark.parametrize("case", ["iho512", "ho256", "iqo513", "qo171"])
 @pytest.mark.parametrize("mode", ["2", "1"])
 def test_two_slot_workgroups_bitwise_equal(monkeypatch, case, mode):

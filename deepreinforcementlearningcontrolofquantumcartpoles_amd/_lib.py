@@ -30,7 +30,7 @@ EXPORTS = (
     "qc_set_stream", "qc_sync", "qc_set_seed", "qc_set_step_counter", "qc_get_step_counter",
     "qc_env_counters", "qc_set_seed_mt19937", "qc_noise_mode", "qc_mt19937_state", "qc_mt19937_words",
     "qc_set_dynamics", "qc_add_force", "qc_step", "qc_moments", "qc_x_expectation", "qc_outside_prob",
-    "qc_boundary_fail", "qc_energy", "qc_phonon_number", "qc_reset", "qc_control", "qc_record_row_len", "qc_record",
+    "qc_boundary_fail", "qc_energy", "qc_hamiltonian_dot_psi", "qc_phonon_number", "qc_reset", "qc_control", "qc_record_row_len", "qc_record",
     "qc_scan_levels", "qc_take_errors", "qc_step_group_size", "qc_group_layout", "qc_wavefunction_len", "qc_wavefunction_obs", "qc_set_timing", "qc_step_kernel_time",
     "qc_actor_create", "qc_actor_destroy", "qc_actor_last_error", "qc_actor_set_stream", "qc_actor_load",
     "qc_actor_noise_len", "qc_actor_act",
@@ -222,6 +222,7 @@ def lib() -> ctypes.CDLL:
     L.qc_outside_prob.argtypes = [vp, vp, d, vp]
     L.qc_boundary_fail.argtypes = [vp, vp, vp]
     L.qc_energy.argtypes = [vp, vp, vp]
+    L.qc_hamiltonian_dot_psi.argtypes = [vp, vp]
     L.qc_phonon_number.argtypes = [vp, vp, vp]
     L.qc_reset.argtypes = [vp, vp, i32, vp, d, d, d, vp, vp, vp]
     L.qc_control.argtypes = [vp, vp, i32, d, d, d, vp, vp]

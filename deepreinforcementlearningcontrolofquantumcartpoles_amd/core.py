@@ -286,6 +286,12 @@ class Stepper:
         L.check(L.lib().qc_energy(self._h, _ptr(psi), _ptr(out)), self._h)
         return out
 
+    def hamiltonian_dot_psi(self, psi: torch.Tensor) -> None:
+        """psi <- H psi in place (the force-free Hamiltonian; the reference's Hamiltonian_dot_psi)."""
+        self._check_psi(psi)
+        self._bind_stream()
+        L.check(L.lib().qc_hamiltonian_dot_psi(self._h, _ptr(psi)), self._h)
+
     def phonon_number(self, psi: torch.Tensor) -> torch.Tensor:
         self._check_psi(psi)
         out = torch.empty((self.batch,), dtype=torch.float64, device=self.device)

@@ -765,6 +765,15 @@ int qc_energy(qc_handle* h, const void* psi, double* out) {
     return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
 }
 
+int qc_hamiltonian_dot_psi(qc_handle* h, void* psi) {
+    if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
+    KArgs a = base_args(h);
+    a.psi = (double*)psi;
+    DeviceGuard g(h->device);
+    int rc = launch_aux(h->p.family, h->R, 5, a, 0.0, nullptr, h->stream);
+    return rc ? fail(h, rc, "aux kernel launch failed") : QC_OK;
+}
+
 int qc_phonon_number(qc_handle* h, const void* psi, double* out) {
     if (!h || (!psi && h->p.batch > 0)) return QC_EINVAL;
     if (!h->op.fock) return fail(h, QC_EINVAL, "phonon number is defined on Fock families");

@@ -2166,7 +2166,8 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
 }
 
 // what: 0 = x_expectation (double), 1 = outside probability (double), 2 = boundary Fail (int32),
-//       3 = energy Re<psi|H|psi> w at F = 0 (double), 4 = Fock phonon number sum n |psi_n|^2 (double)
+//       3 = energy Re<psi|H|psi> w at F = 0 (double), 4 = Fock phonon number sum n |psi_n|^2 (double),
+//       5 = psi <- H psi in place with the force-free H (Hamiltonian_dot_psi; out unused)
 template <int FAM, int R, typename RT = double>
 __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth, void* out) {
     const int lane = threadIdx.x & 63;
@@ -2179,6 +2180,18 @@ __global__ __launch_bounds__(256) void k_aux(const KArgs a, int what, double xth
     cd psi[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? ld_psi<RT>(a.psi, e0 + base + j) : C(0.0, 0.0);
+    if (what == 5) {   // (every lane holds its rows in registers before any lane writes: in place is safe)
+        cd hp[R];
+        apply_h<FAM, R>(psi, hp, cf, lane);
+        RT* q = (RT*)a.psi;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            if (base + j < N) {
+                q[2 * (e0 + base + j)] = (RT)hp[j].re;
+                q[2 * (e0 + base + j) + 1] = (RT)hp[j].im;
+            }
+        return;
+    }
     double s[3] = {0.0, 0.0, 0.0};
     if (what == 0) {
         cd xp[R];

@@ -158,6 +158,23 @@ class _Simulation:
         self._psi.copy_(self._torch.from_numpy(state).view(1, -1))
         return float(self._st.x_expectation(self._psi)[0])
 
+    # Hamiltonian_dot_psi(state): IHO/simulation_i.cpp:585-601, HO/simulation.cpp:566-582 — state <- H state in
+    # place with the force-free Hamiltonian (mkl_sparse_z_mv of harmonic_Hamil); returns 0.0 like the reference
+    def Hamiltonian_dot_psi(self, state):
+        _check_state(state, self.N)
+        self._psi.copy_(self._torch.from_numpy(state).view(1, -1))
+        self._st.hamiltonian_dot_psi(self._psi)
+        state[:] = self._psi[0].cpu().numpy()
+        return 0.0
+
+    # solve_ab(state): IHO/simulation_i.cpp:603-616, HO/simulation.cpp:584-598 — not reproduced: the IHO module
+    # calls LAPACKE_zgbtrs with kl = ku = 1 on its kl = ku = 2 factorisation (a different, ill-defined operator) and
+    # no driver calls it
+    def solve_ab(self, state):
+        _check_state(state, self.N)
+        raise NotImplementedError("solve_ab is not reproduced (a debugging entry point of the reference modules that "
+                                  "no driver calls; the IHO module's zgbtrs call uses the wrong band widths)")
+
     # get_moments(state, data): QO/simulation_quart.cpp:363-388 (grid families only in the reference)
     def get_moments(self, state, data):
         _check_state(state, self.N)
@@ -386,6 +403,10 @@ def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", s
             setattr(mod, name, getattr(sim, name))
         if not phys.fock:
             mod.get_moments = sim.get_moments
+        elif server is None:
+            # the Fock modules' method tables (IHO/simulation_i.cpp:618-631, HO/simulation.cpp:599-612)
+            mod.Hamiltonian_dot_psi = sim.Hamiltonian_dot_psi
+            mod.solve_ab = sim.solve_ab
         mod._impl = sim
         _MODULES[key] = mod
     return _MODULES[key]

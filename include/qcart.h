@@ -201,6 +201,11 @@ int qc_boundary_fail(qc_handle* h, const void* psi, int32_t* out);
  * force-free H: out [B] */
 int qc_energy(qc_handle* h, const void* psi, double* out);
 
+/* Hamiltonian_dot_psi(state) (IHO/simulation_i.cpp:585-601, HO/simulation.cpp:566-582): psi <- H psi in place for
+ * every env, H the force-free Hamiltonian (mkl_sparse_z_mv of harmonic_Hamil; grid families: their kinetic +
+ * potential H, which the reference's grid modules do not export) */
+int qc_hamiltonian_dot_psi(qc_handle* h, void* psi);
+
 /* phonon_number(state) (HO/main_parallel.py:88-89, harmonic-cooling reward) = sum n |psi_n|^2: out [B] */
 int qc_phonon_number(qc_handle* h, const void* psi, double* out);
 

@@ -37,6 +37,22 @@ def test_simulation_dropin_matches_oracle(oracle_mod):
     assert isinstance(q, float) and isinstance(xm, float) and isinstance(fail, int)
 
 
+@pytest.mark.parametrize("family, n_max", [(cfg.IHO, 63), (cfg.HO, 40)])
+def test_simulation_dropin_hamiltonian_dot_psi(oracle_mod, family, n_max):
+    """Hamiltonian_dot_psi(state) (IHO/simulation_i.cpp:585-601, HO/simulation.cpp:566-582): state <- H state in
+    place with the force-free H, returns 0.0 — against the oracle's dense H. solve_ab is refused with its reason."""
+    sim = S.load(family, n_max=n_max)
+    o = oracle_mod.OracleSystem(family, n_max=n_max, omega=cfg.DEFAULTS[family].omega)
+    rng = np.random.default_rng(2)
+    state = rng.standard_normal(n_max + 1) + 1j * rng.standard_normal(n_max + 1)
+    state[20:] = 0
+    want = o.dense_h() @ state
+    assert sim.Hamiltonian_dot_psi(state) == 0.0
+    np.testing.assert_allclose(state, want, rtol=1e-13, atol=1e-13)
+    with pytest.raises(NotImplementedError, match="solve_ab"):
+        sim.solve_ab(state)
+
+
 def test_simulation_dropin_errors_like_reference():
     sim = S.load(cfg.IHO, n_max=63)
     with pytest.raises(ValueError, match="required size 64"):

@@ -119,3 +119,14 @@ extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
 #define QC_SOLVE_STAMP_ARGS
 #define QC_SOLVE_STAMP_PASS
 #endif
+
+// the fp32 R = 32 kernel's mirror bands read in pipelined half-band batches (k_step MPIPE; A/B)
+#ifndef QCART_MPIPE
+#define QCART_MPIPE 1
+#endif
+#ifndef QCART_MPIPE_ROWS
+#define QCART_MPIPE_ROWS 16
+#endif
+#ifndef QCART_MPIPE_DEPTH
+#define QCART_MPIPE_DEPTH 2
+#endif

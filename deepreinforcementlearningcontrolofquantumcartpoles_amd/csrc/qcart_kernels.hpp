@@ -1806,7 +1806,39 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         if constexpr (FAM == 1) {
             // MKL HERMITIAN/UPPER mirror: A_eff = A - 2i tril(Im A, -1)  (SURVEY App. C H1); the band
             // reads go in batches of MB bands fenced from the arithmetic so each batch is in flight at once
-            if (a.mirror) {
+            // MPIPE (the fp32 R = 32 kernel, one wave per SIMD: nothing else hides the LDS latency): the bands in
+            // batches of QCART_MPIPE_ROWS reads, each batch's reads issued QCART_MPIPE_DEPTH - 1 batches before its
+            // multiply-adds — half bands two deep: the same 32 registers of read buffer as one fenced band, and the
+            // reads of one batch run under the other's FMAs (C5 41.77 -> 41.35 ms, two same-call pairs)
+            constexpr bool MPIPE = sizeof(RT) == 4 && R >= 32 && QCART_MPIPE;
+            if (a.mirror && MPIPE) {
+                constexpr int HB = QCART_MPIPE_ROWS, NB = 10 * R / HB, DP = QCART_MPIPE_DEPTH;
+                static_assert(!MPIPE || (R % HB == 0 && DP >= 2), "mirror batches: whole fractions of a band");
+                cx<RT> lo[10];
+                make_lo<R, 10>(D1, lo, lnv);
+                RT mb[DP][HB];
+                auto rd = [&](int q, RT (&dst)[HB]) {   // batch q: band q HB / R, rows (q HB) % R ..
+#pragma unroll
+                    for (int i = 0; i < HB; ++i)
+                        dst[i] = tb.d(SL.m2 + (uint32_t)((q * HB / R) * R + (q * HB) % R + i) * CR);
+                };
+#pragma unroll
+                for (int q = 0; q < DP - 1; ++q) rd(q, mb[q]);
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    if (q + DP - 1 < NB) rd(q + DP - 1, mb[(q + DP - 1) % DP]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int d = q * HB / R + 1;
+#pragma unroll
+                    for (int i = 0; i < HB; ++i) {
+                        const int j = (q * HB) % R + i;
+                        const RT m = mb[q % DP][i];
+                        const cx<RT> dv = (j - d >= 0) ? D1[(j - d) >= 0 ? (j - d) : 0]
+                                                   : lo[(10 + j - d) < 10 ? (10 + j - d) : 0];
+                        acc[j] = C(acc[j].re + m * dv.im, acc[j].im - m * dv.re);
+                    }
+                }
+            } else if (a.mirror) {
                 constexpr int MB = 1;   // bands per batch of reads (fp32 R = 32 with 2: 42.4 -> 50.7 ms, spills)
                 cx<RT> lo[10];
                 make_lo<R, 10>(D1, lo, lnv);

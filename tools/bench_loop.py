@@ -33,11 +33,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--capacity", type=int, default=0)   # xp: 7000 x 18 x 100 (IHO/arguments.py:80, main_parallel.py:595)
     ap.add_argument("--input", choices=("xp", "measurements"), default="xp")
-    ap.add_argument("--reset", choices=("immediate", "deferred"), default="immediate",
-                    help="BatchedEnv auto-reset mode (deferred: finished envs reset in the next call's launch, no host sync)")
+    ap.add_argument("--reset", choices=("immediate", "deferred"), default=None,
+                    help="BatchedEnv auto-reset mode (deferred: finished envs reset in the next call's launch, no host "
+                         "sync; the default for 'xp', where it applies; immediate for 'measurements')")
     ap.add_argument("--marker", action="store_true",
                     help="wrap the timed steps in a roctx range 'timed' (tools/loop_breakdown.py, rocprofv3 --marker-trace)")
     args = ap.parse_args()
+    if args.reset is None:
+        args.reset = "deferred" if args.input == "xp" else "immediate"
     B = args.batch
     meas = args.input == "measurements"
     ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=511)

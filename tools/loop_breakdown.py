@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--input", default="xp")
-    ap.add_argument("--reset", default="immediate", choices=("immediate", "deferred"))
+    ap.add_argument("--reset", default="deferred", choices=("immediate", "deferred"))
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out", "loop_bd"))
     a = ap.parse_args()

@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,7 +32,8 @@ struct qcc {
     double* psi;   /* this slot's state row [2N] */
     double* obs;   /* this slot's observation row [QCS_MAX_OBS] */
     int index;
-    double spin_s;   /* how long a call polls its done word before sleeping on the tick word */
+    double spin_s;   /* how long a call polls its done word before sleeping on the tick word (< 0: adaptive) */
+    int cpus;        /* usable host CPUs (affinity mask, capped by the cgroup CPU quota) */
     char err[160];
 };
 
@@ -39,6 +41,23 @@ static char g_err[160];
 
 static void set_err(qcc* c, const char* m) {
     snprintf(c ? c->err : g_err, sizeof(g_err), "%s", m);
+}
+
+/* usable CPUs: the affinity mask, capped by a cgroup v2 CPU quota (cpu.max "quota period") */
+static int usable_cpus(void) {
+    cpu_set_t set;
+    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+    FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char q[32] = {0};
+        long period = 0;
+        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long lim = (atol(q) + period - 1) / period;
+            if (lim > 0 && lim < n) n = (int)lim;
+        }
+        fclose(f);
+    }
+    return n < 1 ? 1 : n;
 }
 
 static double now_s(void) {
@@ -97,7 +116,8 @@ int qcc_open(const char* name, qcc** out) {
     {
         /* QCC_SPIN_US: a tick is tens of microseconds, a futex wake-up adds its own; the default polls for 150 us */
         const char* v = getenv("QCC_SPIN_US");
-        c->spin_s = (v && *v ? atof(v) : 150.0) * 1e-6;
+        c->spin_s = v && *v ? atof(v) * 1e-6 : -1.0;
+        c->cpus = usable_cpus();
     }
     c->psi = (double*)(m + h->psi_off) + (size_t)idx * 2 * (size_t)h->N;
     c->obs = (double*)(m + h->obs_off) + (size_t)idx * QCS_MAX_OBS;
@@ -160,7 +180,12 @@ static int call(qcc* c) {
         __atomic_add_fetch(&h->kick, 1u, __ATOMIC_SEQ_CST);
         syscall(SYS_futex, &h->kick, FUTEX_WAKE, 1, NULL, NULL, 0);
     }
-    /* a short spin (a tick takes tens of microseconds), then sleep on the tick word */
+    /* a short spin (a tick takes tens of microseconds), then sleep on the tick word. Adaptive (no QCC_SPIN_US):
+     * 150 us while every attached client has a CPU of its own, 20 us once they outnumber the usable CPUs — the
+     * reference's 30-40 actors on a 16-CPU share: spinning clients would take the CPU from the ones whose tick
+     * has completed (P = 32: 4.6e5 vs 3.6e5 step calls/s, P = 40: 5.3e5 vs 3.2e5) */
+    double spin = c->spin_s;
+    if (spin < 0) spin = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) <= c->cpus ? 150e-6 : 20e-6;
     const double t0 = now_s();
     for (int i = 0;; ++i) {
         if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) {
@@ -168,7 +193,7 @@ static int call(qcc* c) {
             return s->status;
         }
         __builtin_ia32_pause();
-        if ((i & 31) == 31 && now_s() - t0 > c->spin_s) break;
+        if ((i & 31) == 31 && now_s() - t0 > spin) break;
     }
     for (;;) {
         __atomic_store_n(&s->waiting, 1u, __ATOMIC_SEQ_CST);

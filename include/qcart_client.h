@@ -11,9 +11,10 @@
  * All state pointers are HOST pointers: psi = one env's complex128 state, [N] interleaved (re, im), mutated in
  * place like the reference's numpy `state`. Return value 0 on success, < 0 on error; qcc_last_error explains.
  *
- * A call copies the state into the slot's row, publishes the request and polls its done word for QCC_SPIN_US
- * microseconds (environment variable read at qcc_open, default 150: a tick takes tens of microseconds) before
- * sleeping on the server's tick futex. P spinning clients plus the server thread need P + 1 cores.
+ * A call copies the state into the slot's row, publishes the request and polls its done word before sleeping on
+ * the server's tick futex: QCC_SPIN_US microseconds (environment variable read at qcc_open), by default 150 while
+ * the attached clients have a usable CPU each (affinity mask capped by the cgroup CPU quota) and 20 once they
+ * outnumber them (spinning clients would take the CPU from those whose tick has completed).
  */
 #ifndef QCART_CLIENT_H
 #define QCART_CLIENT_H

@@ -11,7 +11,9 @@
 // (dt, gamma) — each group one qc_step with a per-env step budget (env_steps: the others stay frozen) — then
 // x_expectation / moments over the batch; one stream synchronisation; results back into the slots; done = req.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <linux/futex.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
@@ -329,6 +331,22 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
     if (wake) futex_wake(&s->hdr->tick, 1 << 30);
 }
 
+// slots whose client process has exited without qcc_close (killed actor): released, so that the batching wait
+// does not hold every tick for a request that never comes (a pending one is dropped)
+void reap_dead_clients(qc_server* s) {
+    for (int e = 0; e < s->P; ++e) {
+        qcs_slot& sl = s->slots[e];
+        const int32_t pid = __atomic_load_n(&sl.pid, __ATOMIC_ACQUIRE);
+        if (!ld_acq(&sl.owner) || pid <= 0) continue;
+        if (kill(pid, 0) == 0 || errno != ESRCH) continue;
+        s->served[e] = __atomic_load_n(&sl.req, __ATOMIC_ACQUIRE);
+        __atomic_store_n(&sl.done, s->served[e], __ATOMIC_RELEASE);
+        __atomic_store_n(&sl.pid, 0, __ATOMIC_RELAXED);
+        __atomic_sub_fetch(&s->hdr->n_clients, 1u, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&sl.owner, 0u, __ATOMIC_RELEASE);
+    }
+}
+
 void scan(qc_server* s, std::vector<int>& pend, int& owned) {
     pend.clear();
     owned = 0;
@@ -460,8 +478,12 @@ int qc_server_run(qc_server* s, double seconds) {
     const double t_end = seconds > 0 ? now_us() + seconds * 1e6 : 1e300;
     std::vector<int> pend;
     int owned = 0;
-    double idle_since = now_us();
+    double idle_since = now_us(), last_reap = now_us();
     while (!s->stop.load(std::memory_order_relaxed) && now_us() < t_end) {
+        if (now_us() - last_reap > 100000.0) {   // every 0.1 s
+            reap_dead_clients(s);
+            last_reap = now_us();
+        }
         scan(s, pend, owned);
         if (pend.empty()) {
             if (now_us() - idle_since < 200.0) {   // short spin: the next request is usually microseconds away

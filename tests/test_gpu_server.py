@@ -19,6 +19,8 @@ from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as
 
 from tests import test_gpu_noise as TN  # noqa: E402
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 _N = [0]
 
 
@@ -203,3 +205,42 @@ def test_served_errors():
         srv.close()
     with pytest.raises(RuntimeError, match="no step server"):
         S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name)
+
+
+def test_killed_client_slot_is_released():
+    """An actor process killed without closing its module (no qcc_close) holds its slot until the server sees the
+    process gone (checked every 0.1 s): then the slot is free again for a new actor."""
+    import subprocess
+    import sys
+    import time
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=1, name=name, n_max=63).start()
+    try:
+        code = ("import sys, time; sys.path.insert(0, %r)\n"
+                "from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg, simulation as S\n"
+                "m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), %r)\n"
+                "print('ready', flush=True); time.sleep(60)\n") % (ROOT, name)
+        p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+        try:
+            assert p.stdout.readline().startswith("ready")
+            with pytest.raises(RuntimeError, match="slots are taken"):
+                S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name)
+        finally:
+            p.kill()
+            p.wait()
+        m = None
+        for _ in range(50):
+            try:
+                m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name)
+                break
+            except RuntimeError:
+                time.sleep(0.05)
+        assert m is not None, "the killed client's slot was not released"
+        st = np.zeros(64, np.complex128)
+        st[0] = 1
+        q, xm, fail = m.step(st, 1 / 1440, 0.0, 2 * pi)
+        assert fail == 0 and np.isfinite(q)
+        m.close()
+    finally:
+        srv.close()
+

@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=20)   # ~0.5 s: a fresh box ramps its clock over the first launches
     ap.add_argument("--capacity", type=int, default=0)   # xp: 7000 x 18 x 100 (IHO/arguments.py:80, main_parallel.py:595)
     ap.add_argument("--input", choices=("xp", "measurements"), default="xp")
     ap.add_argument("--reset", choices=("immediate", "deferred"), default=None,

@@ -132,8 +132,8 @@ int qc_set_seed_mt19937(qc_handle* h, const uint32_t* seeds);
  * actor process's set_seed under the step server (qc_server_*). Needs the handle in MT19937 mode. */
 int qc_set_seed_mt19937_envs(qc_handle* h, const uint32_t* seeds, const uint8_t* mask);
 int qc_noise_mode(const qc_handle* h);
-/* the next normals of every env's MT19937 stream into `noise` (device double [n_steps][B][2], qc_step's injected
- * layout): min(n_steps, env_steps[e]) steps for env e (env_steps NULL: n_steps each), the stream advancing by the
+/* the next normals of every env's MT19937 stream (the reference's vdRngGaussian draws, IHO/simulation_i.cpp:435)
+ * into `noise` (device double [n_steps][B][2], qc_step's injected layout): min(n_steps, env_steps[e]) steps for env e (env_steps NULL: n_steps each), the stream advancing by the
  * words drawn — what qc_step draws itself when it is given no noise. With pre / has_pre (device double [B][2], uint8
  * [B]; both or neither) an env with has_pre[e] != 0 has already drawn its next step's pair into pre[e] (an earlier
  * call with n_steps = 1): it becomes step 0 and only the remaining steps are drawn. The step server prefetches each

@@ -46,26 +46,87 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every usable host core (affinity / cgroup quota)")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="bench.py's own launcher: kill every rank after this many seconds (0: no limit)")
+    ap.add_argument("--digest-envs", type=int, default=0,
+                    help="report sha256 digests of the final state per run of this many envs (shard checks)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: the ranks join a gloo group and report the world size")
     return ap.parse_args()
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, deadline_s: float = 0.0) -> int:
     """--gpus N without WORLD_SIZE in the environment: start N copies of this script as ranks 0..N-1
-    (LOCAL_RANK = rank, one GPU each), before this process touches any GPU, and return the worst exit
-    code. Rank 0 prints the JSON line. The driver's torchrun launch sets WORLD_SIZE and skips this."""
+    (LOCAL_RANK = rank, one GPU each), before this process touches any GPU. Rank 0 prints the JSON line.
+    The ranks are polled together (IHO/main_parallel.py:345-359 starts its workers the same way and would
+    otherwise wait on a dead one forever): the first rank to exit non-zero has its siblings killed, its
+    stderr tail repeated and its code returned, so a rank that dies in RCCL init ends the job in seconds
+    instead of leaving the others blocked in the rendezvous. deadline_s > 0 bounds the whole job the same
+    way (code 124). The driver's torchrun launch sets WORLD_SIZE and skips this."""
+    import collections
     import socket
     import subprocess
+    import threading
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    procs = []
+    procs, tails, pumps = [], [], []
+
+    def pump(stream, tail):
+        # forward the rank's stderr line by line and keep its last lines for the failure report
+        for line in iter(stream.readline, b""):
+            tail.append(line.decode(errors="replace"))
+            sys.stderr.write(line.decode(errors="replace"))
+            sys.stderr.flush()
+        stream.close()
+
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    return max(abs(p.wait()) for p in procs)
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             stderr=subprocess.PIPE)
+        tail = collections.deque(maxlen=40)
+        th = threading.Thread(target=pump, args=(p.stderr, tail), daemon=True)
+        th.start()
+        procs.append(p)
+        tails.append(tail)
+        pumps.append(th)
+
+    def code_of(rc):
+        return rc if rc >= 0 else 128 - rc       # killed by signal s: the shell's 128 + s
+
+    t0 = time.monotonic()
+    failed, rc_fail = None, 0
+    while True:
+        live = [p for p in procs if p.poll() is None]
+        bad = [r for r, p in enumerate(procs) if p.returncode not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            rc_fail = code_of(procs[failed].returncode)
+            break
+        if not live:
+            break
+        if deadline_s and time.monotonic() - t0 > deadline_s:
+            failed, rc_fail = -1, 124
+            break
+        time.sleep(0.05)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+    for th in pumps:
+        th.join(timeout=5)
+    if failed is None:
+        return 0
+    if failed < 0:
+        sys.stderr.write(f"bench.py: ranks still running after {deadline_s:.0f} s; all ranks killed\n")
+    else:
+        sys.stderr.write(f"bench.py: rank {failed} of {n} exited with code {rc_fail}; the other ranks were "
+                         f"killed. Its stderr tail:\n" + "".join(tails[failed]))
+    sys.stderr.flush()
+    return rc_fail
 
 
 def cpu_baseline(config: str, seconds: float, threads: int):
@@ -144,7 +205,8 @@ def dry_run(world: int, rank: int):
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")
+        from deepreinforcementlearningcontrolofquantumcartpoles_amd import distributed as D
+        D.init_from_env("gloo")
     t = torch.ones(1)
     if world > 1:
         dist.all_reduce(t)
@@ -152,6 +214,40 @@ def dry_run(world: int, rank: int):
         print(json.dumps({"dry_run": True, "n_gpus": world, "world_size_seen": int(t.item())}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+M32 = 0xFFFFFFFF
+
+
+def _hash32(x):
+    """A 32-bit integer mix (two xorshift-multiply rounds) on an int64 tensor of values < 2^32; every
+    intermediate product stays below 2^63."""
+    x = ((x >> 16) ^ x) * 0x45D9F3B & M32
+    x = ((x >> 16) ^ x) * 0x45D9F3B & M32
+    return (x >> 16) ^ x
+
+
+def synth_inputs(n_ctrl: int, B: int, offset: int, n_actions: int, dev):
+    """Synthetic actions [n_ctrl][B] ~ U{0..n_actions-1} and Gaussian-packet parameters, keyed by the GLOBAL
+    env id (offset + e) and the control step, so a rank's shard sees exactly the inputs of the same envs in a
+    one-rank run of the whole batch (the Philox noise and psi0 are keyed the same way: env_offset)."""
+    import torch
+    gid = torch.arange(offset, offset + B, dtype=torch.int64, device=dev)
+    k = torch.arange(n_ctrl, dtype=torch.int64, device=dev)
+    x = (gid[None, :] * 0x9E3779B1 + k[:, None] * 0x85EBCA6B + 0x2545F491) & M32
+    acts = (_hash32(x) % n_actions).to(torch.int32)
+
+    def uniform(salt):
+        return _hash32((gid * 0x9E3779B1 + salt) & M32).to(torch.float64) * 2.0 ** -32
+
+    return acts.contiguous(), uniform(0x68E31DA4), uniform(0xB5297A4D), uniform(0x1B56C4E9)
+
+
+def psi_digests(psi, chunk: int):
+    """sha256 (16 hex digits) of the state's bytes per run of `chunk` envs, in env order."""
+    import hashlib
+    h = psi.cpu().contiguous().numpy()
+    return [hashlib.sha256(h[i:i + chunk].tobytes()).hexdigest()[:16] for i in range(0, h.shape[0], chunk)]
 
 
 def main():
@@ -162,14 +258,23 @@ def main():
     use_dist = world > 0
     if world == 0:
         if args.gpus > 1:
-            sys.exit(launch_ranks(args.gpus))
+            sys.exit(launch_ranks(args.gpus, args.launch_timeout))
         world = 1
     elif world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # fault injection for the launcher tests: this rank exits at once with code 3 (or hangs)
+    if os.environ.get("QCART_BENCH_FAIL_RANK", "") == str(rank):
+        sys.stderr.write(f"bench.py rank {rank}: QCART_BENCH_FAIL_RANK, exiting with 3\n")
+        sys.exit(3)
+    if os.environ.get("QCART_BENCH_HANG_RANK", "") == str(rank):
+        time.sleep(3600)
     if args.dry_run:
         return dry_run(world, rank)
+    # rehearsal of the N-rank path on a one-GPU lease: every rank steps its shard on device 0 and gloo carries
+    # the collectives (RCCL refuses two ranks on one device); timing, sharding and gathers are the N-GPU job's
+    share = os.environ.get("QCART_BENCH_SHARE_DEVICE", "0") == "1"
 
     import torch
     import torch.distributed as dist
@@ -178,11 +283,18 @@ def main():
     from deepreinforcementlearningcontrolofquantumcartpoles_amd import distributed as D
     from deepreinforcementlearningcontrolofquantumcartpoles_amd.core import Stepper
 
-    if use_dist:
+    if use_dist and share:
+        torch.cuda.set_device(0)
+        D.init_from_env("gloo")
+    elif use_dist:
         D.init_from_env("nccl")              # RCCL (torch.distributed "nccl" on ROCm), one rank per GPU
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if use_dist else 0)
+    dev = torch.device("cuda", local if (use_dist and not share) else 0)
+
+    def coll(x):
+        # gloo (the rehearsal) takes host tensors
+        return x.cpu() if share else x
 
     conf = cfg.BENCH_CONFIGS[args.config]
     ph = conf["physics"]
@@ -190,17 +302,11 @@ def main():
     n_sub = args.sub_steps or ph.control_interval
     st = Stepper(ph, B, dev, seed=42, env_offset=rank * B)
     psi = st.new_state()
+    acts_all, u0, u1, u2 = synth_inputs(args.steps + args.warmup, B, rank * B, ph.n_actions, dev)
     if ph.fock:
         st.reset(psi, 1, arg0=16)       # synthetic psi0: random amplitudes on levels < 16
     else:
-        g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-        k = (torch.rand(B, generator=g, dtype=torch.float64) * 0.6 - 0.3).to(dev)
-        mu = (torch.rand(B, generator=g, dtype=torch.float64) * 2 - 1).to(dev)
-        sg = (torch.rand(B, generator=g, dtype=torch.float64) * 0.6 + 0.7).to(dev)
-        st.reset(psi, 2, k=k, mean=mu, std=sg)
-    gen = torch.Generator(device=dev).manual_seed(7 + rank)
-    acts_all = torch.randint(0, ph.n_actions, (args.steps + args.warmup, B), generator=gen, device=dev,
-                             dtype=torch.int32)
+        st.reset(psi, 2, k=u0 * 0.6 - 0.3, mean=u1 * 2 - 1, std=u2 * 0.6 + 0.7)
 
     def one(k):
         return st.step(psi, acts_all[k], n_sub, want_fail=True, want_obs=True, want_term=(ph.family == 3))
@@ -226,15 +332,21 @@ def main():
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     world_seen = 1
     rccl = None
+    digests = psi_digests(psi, args.digest_envs) if args.digest_envs else None
     if use_dist:
+        t = coll(t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         world_seen = dist.get_world_size()
         # RCCL gather of per-env episode statistics after the timed region (distributed.gather_episode_stats,
         # device tensors): each env's survival through the last control step and its first Fail step
         survived = (out["fail_step"] == 0).to(torch.float64)
-        R, L = D.gather_episode_stats(survived, out["fail_step"].to(torch.float64))
+        R, L = D.gather_episode_stats(coll(survived), coll(out["fail_step"].to(torch.float64)))
         rccl = {"backend": dist.get_backend(), "world_size": world_seen, "gathered_envs": int(R.numel()),
-                "gathered_survivors": float(R.sum().item()), "device": str(R.device)}
+                "gathered_survivors": float(R.sum().item()), "device": str(R.device), "share_device": share}
+        if digests is not None:
+            every = [None] * world_seen
+            dist.all_gather_object(every, digests)
+            digests = [d for r in every for d in r]
     elapsed, kern_ms = float(t[0]), float(t[1])
     sha = lib_sha()
     units = B * world * n_sub * args.steps
@@ -265,6 +377,7 @@ def main():
                                f"{n_sub} physics steps + moments per step ({args.config})",
                    "global_batch": B * world, "seq_len": N, "parallelism": f"env-shard{world}",
                    "physics_steps_per_step": n_sub, "world_size_seen": world_seen, "rccl": rccl},
+        "psi_digests": digests,
         # bound / achieved / peak / frac: the north-star HBM yardstick — algorithmic psi bytes (read + write
         # per physics step) per k_step launch / the launch's time, against the HBM peak. What actually binds
         # k_step is the FP vector pipe (psi stays in VGPRs across the fused steps): that roofline is the

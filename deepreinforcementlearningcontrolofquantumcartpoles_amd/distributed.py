@@ -9,6 +9,7 @@ a few KB, latency-bound.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from typing import Tuple
 
@@ -24,6 +25,11 @@ def shard(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
     count = base + (1 if rank < extra else 0)
     offset = rank * base + min(rank, extra)
     return offset, count
+
+
+# rendezvous and collective timeout: a rank that never joins (it died in RCCL init, or its GPU is gone) fails the
+# others in bounded time instead of leaving them blocked for torch's 10-minute default
+INIT_TIMEOUT_S = float(os.environ.get("QCART_DIST_TIMEOUT_S", "120"))
 
 
 def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
@@ -42,9 +48,10 @@ def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(seconds=INIT_TIMEOUT_S))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=datetime.timedelta(seconds=INIT_TIMEOUT_S))
     return world, rank, local
 
 

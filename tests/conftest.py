@@ -1,5 +1,4 @@
 import os
-import socket
 import subprocess
 import sys
 import tempfile
@@ -10,8 +9,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-RCCL_BATCH = 512
-
 
 def _selects_gpu(config) -> bool:
     m = (config.getoption("markexpr", "") or "").replace(" ", "")
@@ -19,19 +16,15 @@ def _selects_gpu(config) -> bool:
 
 
 def _start_rccl_child(config):
-    """tests/test_gpu_rccl.py: bench.py's rank body under a launcher's environment at WORLD_SIZE = 1 (an RCCL
-    communicator of one rank). Started here, before collection imports any module that initialises the GPU
-    in this process, so the child is a fresh program started by a process that never touched the GPU."""
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    out = tempfile.NamedTemporaryFile(prefix="qcart_rccl_", suffix=".log", delete=False)
-    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
-               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = ["timeout", "-k", "10", "300", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1",
-           "--steps", "3", "--warmup", "1", "--batch", str(RCCL_BATCH), "--no-cpu-baseline"]
-    proc = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=out, stderr=subprocess.STDOUT)
-    config._qcart_rccl = (proc, out.name)
+    """tests/test_gpu_rccl.py: the bench.py runs of tests/bench_children.py (RCCL at world 1, the two-rank
+    launcher rehearsal on one device, the one-rank whole batch). Started here, before collection imports any
+    module that initialises the GPU in this process, so every child is a fresh program started by a process
+    that never touched the GPU."""
+    outdir = tempfile.mkdtemp(prefix="qcart_bench_children_")
+    log = open(os.path.join(outdir, "runner.log"), "w")
+    proc = subprocess.Popen([sys.executable, "-m", "tests.bench_children", outdir], cwd=ROOT, stdout=log,
+                            stderr=subprocess.STDOUT)
+    config._qcart_rccl = (proc, outdir)
 
 
 def pytest_configure(config):
@@ -52,8 +45,12 @@ def pytest_configure(config):
 def _stop_rccl_child(config):
     h = getattr(config, "_qcart_rccl", None)
     if h is not None and h[0].poll() is None:
-        h[0].kill()
-        h[0].wait()
+        h[0].terminate()          # the runner kills its running bench group (tests/bench_children.py)
+        try:
+            h[0].wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            h[0].kill()
+            h[0].wait()
     config._qcart_rccl = None
 
 

@@ -7,7 +7,9 @@ instantiation at its SGPR limit reloading constants from the wrong spill lanes. 
   * every k_step instantiation: no VGPR spills and no scratch, except the documented ones below;
   * two waves per SIMD (8-env workgroups): at most 256 VGPRs (the metric's k_step<1,8,*,double>, C4's grid R = 9,
     C2, the fp32 R <= 16 kernels);
-  * one wave per SIMD: at most 512 VGPRs (C3's grid R = 17, C5's fp32 R = 32, IHO fp64 R = 16).
+  * one wave per SIMD: at most 512 VGPRs (C3's grid R = 17, C5's fp32 R = 32, IHO fp64 R = 16);
+  * SGPR spills (into VGPR lanes: a v_writelane per spill and a v_readlane per reload, on the VALU of a VALU-bound
+    kernel; round 4's wrong-lane reload was one of them): every instantiation at most its SGPR_SPILLS ceiling.
 """
 import os
 import re
@@ -37,6 +39,52 @@ EXCEPTIONS = {
 }
 
 
+# (family, R, MODE, RT, DUAL) -> max sgpr_spill_count. The shipped configs: metric / C2 (1, 8, 2, d, 1), C3 (2, 17, 4,
+# d, 0), C4 (2, 9, 2, d, 1), C5 (1, 32, 1, f, 0), C1 (0, 4, 2, d, 1). The grid kernels keep their uniform step constants
+# device-side (the KAR kernarg re-read measured slower there), so they carry the most. Lower a ceiling
+# when a change lowers the count; raising one needs a measured reason in DESIGN §4.
+SGPR_SPILLS = {
+    (0, 1, 2, "d", 1): 14, (0, 1, 2, "d", 0): 0, (0, 1, 1, "d", 1): 18, (0, 1, 1, "d", 0): 10, (0, 1, 0, "d", 0): 2,
+    (0, 2, 2, "d", 1): 9, (0, 2, 2, "d", 0): 0, (0, 2, 1, "d", 1): 14, (0, 2, 1, "d", 0): 4, (0, 2, 0, "d", 0): 0,
+    (0, 4, 2, "d", 1): 10, (0, 4, 2, "d", 0): 0, (0, 4, 1, "d", 1): 18, (0, 4, 1, "d", 0): 4, (0, 4, 0, "d", 0): 0,
+    (0, 8, 2, "d", 1): 8, (0, 8, 2, "d", 0): 0, (0, 8, 1, "d", 1): 20, (0, 8, 1, "d", 0): 4, (0, 8, 0, "d", 0): 0,
+    (1, 1, 2, "d", 1): 22, (1, 1, 2, "d", 0): 2, (1, 1, 1, "d", 1): 40, (1, 1, 1, "d", 0): 14, (1, 1, 0, "d", 0): 12,
+    (1, 2, 2, "d", 1): 13, (1, 2, 2, "d", 0): 0, (1, 2, 1, "d", 1): 24, (1, 2, 1, "d", 0): 6, (1, 2, 0, "d", 0): 2,
+    (1, 3, 2, "d", 1): 10, (1, 3, 2, "d", 0): 0, (1, 3, 1, "d", 1): 18, (1, 3, 1, "d", 0): 4, (1, 3, 0, "d", 0): 0,
+    (1, 4, 2, "d", 1): 10, (1, 4, 2, "d", 0): 0, (1, 4, 1, "d", 1): 18, (1, 4, 1, "d", 0): 4, (1, 4, 0, "d", 0): 0,
+    (1, 8, 2, "d", 1): 7, (1, 8, 2, "d", 0): 0, (1, 8, 1, "d", 1): 18, (1, 8, 1, "d", 0): 4, (1, 8, 0, "d", 0): 0,
+    (1, 16, 2, "d", 0): 0, (1, 16, 1, "d", 0): 10, (1, 16, 0, "d", 0): 10,
+    (2, 1, 2, "d", 1): 42, (2, 1, 2, "d", 0): 20, (2, 1, 1, "d", 1): 61, (2, 1, 1, "d", 0): 34, (2, 1, 0, "d", 0): 31,
+    (2, 2, 2, "d", 1): 44, (2, 2, 2, "d", 0): 18, (2, 2, 1, "d", 1): 57, (2, 2, 1, "d", 0): 34, (2, 2, 0, "d", 0): 24,
+    (2, 3, 2, "d", 1): 49, (2, 3, 2, "d", 0): 21, (2, 3, 1, "d", 1): 61, (2, 3, 1, "d", 0): 34, (2, 3, 0, "d", 0): 28,
+    (2, 5, 2, "d", 1): 61, (2, 5, 2, "d", 0): 28, (2, 5, 1, "d", 1): 75, (2, 5, 1, "d", 0): 42, (2, 5, 0, "d", 0): 44,
+    (2, 9, 2, "d", 1): 81, (2, 9, 2, "d", 0): 44, (2, 9, 1, "d", 1): 99, (2, 9, 1, "d", 0): 57, (2, 9, 0, "d", 0): 85,
+    (2, 17, 4, "d", 0): 214, (2, 17, 2, "d", 0): 212, (2, 17, 1, "d", 0): 279, (2, 17, 0, "d", 0): 298,
+    (0, 4, 2, "f", 0): 0, (0, 4, 1, "f", 0): 0, (0, 4, 0, "f", 0): 0,
+    (0, 8, 2, "f", 0): 0, (0, 8, 1, "f", 0): 0, (0, 8, 0, "f", 0): 0,
+    (0, 32, 2, "f", 0): 22, (0, 32, 1, "f", 0): 38, (0, 32, 0, "f", 0): 48,
+    (1, 8, 2, "f", 0): 0, (1, 8, 1, "f", 0): 0, (1, 8, 0, "f", 0): 0,
+    (1, 16, 2, "f", 0): 0, (1, 16, 1, "f", 0): 4, (1, 16, 0, "f", 0): 6,
+    (1, 32, 2, "f", 0): 24, (1, 32, 1, "f", 0): 38, (1, 32, 0, "f", 0): 44,
+}
+
+
+def over_budget(kernels):
+    """The instantiations over any budget: [(key, what, value, limit)]."""
+    bad = []
+    for k, (v, s, scr, sp, ssp) in sorted(kernels.items()):
+        max_sp, max_scr = EXCEPTIONS.get(k, (0, 0))
+        if sp > max_sp:
+            bad.append((k, "vgpr_spill", sp, max_sp))
+        if scr > max_scr:
+            bad.append((k, "scratch", scr, max_scr))
+        if k not in SGPR_SPILLS:
+            bad.append((k, "sgpr_spill (no ceiling)", ssp, None))
+        elif ssp > SGPR_SPILLS[k]:
+            bad.append((k, "sgpr_spill", ssp, SGPR_SPILLS[k]))
+    return bad
+
+
 def step_waves(fam, R, rt):
     """kStepWaves (qcart_kernels.hpp): 8 waves (two per SIMD) where the step fits 256 VGPRs."""
     r_eff = R * (4 if rt == "f" else 8) // 8
@@ -49,11 +97,11 @@ def step_kernels():
         pytest.skip("libqcart.so not built")
     import kernel_resources as K
     out = {}
-    for name, v, s, scr, sp in K.kernels(LIB):
+    for name, v, s, scr, sp, ssp in K.kernels(LIB):
         m = STEP.search(name)
         if m:
             key = (int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4), int(m.group(5)))
-            out[key] = (int(v), int(s), int(scr), int(sp))
+            out[key] = (int(v), int(s), int(scr), int(sp), int(ssp))
     return out
 
 
@@ -68,16 +116,26 @@ def test_every_config_kernel_is_present(step_kernels):
 
 
 def test_step_kernels_do_not_spill(step_kernels):
-    bad = []
-    for k, (v, s, scr, sp) in sorted(step_kernels.items()):
-        max_sp, max_scr = EXCEPTIONS.get(k, (0, 0))
-        if sp > max_sp or scr > max_scr:
-            bad.append((k, sp, scr))
+    bad = over_budget(step_kernels)
     assert not bad, f"(family, R, MODE, RT, DUAL) with spills / scratch over budget: {bad}"
 
 
+def test_budget_check_catches_an_over_budget_entry(step_kernels):
+    """The guard itself: one SGPR spill over C3's ceiling, a VGPR spill in the metric kernel, an instantiation
+    without a ceiling — each is reported."""
+    c3, met = (2, 17, 4, "d", 0), (1, 8, 2, "d", 1)
+    fake = dict(step_kernels)
+    v, s, scr, sp, ssp = fake[c3]
+    fake[c3] = (v, s, scr, sp, SGPR_SPILLS[c3] + 1)
+    v, s, scr, sp, ssp = fake[met]
+    fake[met] = (v, s, scr, EXCEPTIONS[met][0] + 1, ssp)
+    fake[(2, 33, 4, "d", 0)] = (400, 106, 0, 0, 0)
+    whats = {(k, w) for k, w, _, _ in over_budget(fake)}
+    assert whats == {(c3, "sgpr_spill"), (met, "vgpr_spill"), ((2, 33, 4, "d", 0), "sgpr_spill (no ceiling)")}
+
+
 def test_register_budget_matches_waves_per_simd(step_kernels):
-    for (fam, R, mode, rt, dual), (v, s, scr, sp) in step_kernels.items():
+    for (fam, R, mode, rt, dual), (v, s, scr, sp, ssp) in step_kernels.items():
         cap = 256 if step_waves(fam, R, rt) == 8 else 512
         assert v <= cap, ((fam, R, mode, rt, dual), v, cap)
         assert s <= 106, ((fam, R, mode, rt, dual), s)
@@ -85,5 +143,5 @@ def test_register_budget_matches_waves_per_simd(step_kernels):
 
 def test_metric_kernel_budget(step_kernels):
     """The metric kernel (IHO N = 512, two waves per SIMD): <= 256 VGPRs, <= 12 B of scratch."""
-    v, s, scr, sp = step_kernels[(1, 8, 2, "d", 1)]
-    assert v <= 256 and scr <= 12 and sp <= 2
+    v, s, scr, sp, ssp = step_kernels[(1, 8, 2, "d", 1)]
+    assert v <= 256 and scr <= 12 and sp <= 2 and ssp <= 7

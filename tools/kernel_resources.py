@@ -34,7 +34,9 @@ def code_objects(path):
 
 
 def kernels(path):
-    """(name, vgpr_count, sgpr_count, private_segment_fixed_size, vgpr_spill_count) per kernel, as strings."""
+    """(name, vgpr_count, sgpr_count, private_segment_fixed_size, vgpr_spill_count, sgpr_spill_count) per kernel,
+    as strings. sgpr_spill_count: SGPRs the allocator spilled (into VGPR lanes: v_writelane / v_readlane on the VALU,
+    or to scratch when no lane is free)."""
     for co in code_objects(path):
         with tempfile.NamedTemporaryFile(suffix=".co") as f:
             f.write(co)
@@ -48,10 +50,11 @@ def kernels(path):
             def g(k):
                 mm = re.search(r"\." + k + r":\s+(\S+)", b)
                 return mm.group(1) if mm else "?"
-            yield m.group(1), g("vgpr_count"), g("sgpr_count"), g("private_segment_fixed_size"), g("vgpr_spill_count")
+            yield (m.group(1), g("vgpr_count"), g("sgpr_count"), g("private_segment_fixed_size"), g("vgpr_spill_count"),
+                   g("sgpr_spill_count"))
 
 
 if __name__ == "__main__":
     for obj in sys.argv[1:]:
-        for name, v, s, scr, sp in kernels(obj):
-            print(f"{name:48s} vgpr={v:>4} sgpr={s:>4} scratch={scr:>6} vgpr_spill={sp}")
+        for name, v, s, scr, sp, ssp in kernels(obj):
+            print(f"{name:48s} vgpr={v:>4} sgpr={s:>4} scratch={scr:>6} vgpr_spill={sp} sgpr_spill={ssp}")

@@ -34,6 +34,10 @@ void set_create_err(const std::string& s) {
 }
 }  // namespace
 
+namespace qcart {
+void set_global_error(const std::string& m) { set_create_err(m); }
+}  // namespace qcart
+
 struct qc_handle {
     qc_params p{};
     int device = 0;

@@ -60,6 +60,14 @@ static int usable_cpus(void) {
     return n < 1 ? 1 : n;
 }
 
+/* the server is gone: it cleared `alive` (qc_server_destroy), or its process no longer exists (killed, aborted on
+ * a GPU fault: `alive` is never cleared then) */
+static int server_gone(const qcs_header* h) {
+    if (!__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) return 1;
+    const int32_t pid = h->server_pid;
+    return pid > 0 && kill(pid, 0) != 0 && errno == ESRCH;
+}
+
 static double now_s(void) {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
@@ -88,10 +96,18 @@ int qcc_open(const char* name, qcc** out) {
     }
     qcs_header* h = (qcs_header*)m;
     if (h->magic != QCS_MAGIC || h->version != QCS_VERSION || h->total_bytes != (uint64_t)sb.st_size ||
-        !__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) {
+        server_gone(h)) {
         munmap(m, (size_t)sb.st_size);
         close(fd);
-        snprintf(g_err, sizeof(g_err), "%s: no live step server (version / state mismatch)", name);
+        snprintf(g_err, sizeof(g_err), "%s: no live step server (version / state mismatch, or its process exited)",
+                 name);
+        return QCC_ENOSERVER;
+    }
+    if (h->pid_ns != qcs_pid_ns()) {
+        /* pids (the server's liveness check of its clients, and ours of it) mean nothing across PID namespaces */
+        munmap(m, (size_t)sb.st_size);
+        close(fd);
+        snprintf(g_err, sizeof(g_err), "%s: the step server runs in another PID namespace", name);
         return QCC_ENOSERVER;
     }
     qcs_slot* slots = (qcs_slot*)(m + h->slot_off);
@@ -137,9 +153,11 @@ int qcc_open(const char* name, qcc** out) {
 
 void qcc_close(qcc* c) {
     if (!c) return;
-    /* a request still pending is completed first (its slot must not be re-claimed mid-tick) */
+    /* a request still pending is completed first (its slot must not be re-claimed mid-tick), unless the server is
+     * gone; bounded, so a close (also from a destructor) never hangs on a server that stopped answering */
+    const double t0 = now_s();
     while (__atomic_load_n(&c->slot->done, __ATOMIC_ACQUIRE) != __atomic_load_n(&c->slot->req, __ATOMIC_RELAXED) &&
-           __atomic_load_n(&c->hdr->alive, __ATOMIC_ACQUIRE))
+           !server_gone(c->hdr) && now_s() - t0 < 60.0)
         usleep(100);
     c->slot->pid = 0;
     __atomic_sub_fetch(&c->hdr->n_clients, 1u, __ATOMIC_SEQ_CST);
@@ -202,9 +220,10 @@ static int call(qcc* c) {
         struct timespec ts = {0, 20000000L};   /* 20 ms: re-check the server's liveness */
         syscall(SYS_futex, &h->tick, FUTEX_WAIT, t, &ts, NULL, 0);
         if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) break;
-        if (!__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE)) {
+        if (server_gone(h)) {
             __atomic_store_n(&s->waiting, 0u, __ATOMIC_RELAXED);
-            set_err(c, "the step server stopped");
+            set_err(c, __atomic_load_n(&h->alive, __ATOMIC_ACQUIRE) ? "the step server's process exited"
+                                                                    : "the step server stopped");
             return QCC_ENOSERVER;
         }
         if (now_s() - t0 > 600.0) {
@@ -260,5 +279,19 @@ int qcc_moments(qcc* c, const double* psi, double* out) {
     c->slot->op = c->hdr->family >= 2 ? QCS_OP_MOMENTS : QCS_OP_FOCK_OBS;
     const int rc = call(c);
     if (rc == QCC_OK) memcpy(out, c->obs, sizeof(double) * (size_t)c->hdr->n_obs);
+    return rc;
+}
+
+int qcc_hamiltonian_dot_psi(qcc* c, double* psi) {
+    if (!c || !psi) return QCC_EINVAL;
+    if (c->hdr->family >= 2) {
+        set_err(c, "Hamiltonian_dot_psi is a Fock-module function");
+        return QCC_EINVAL;
+    }
+    const size_t bytes = sizeof(double) * 2 * (size_t)c->hdr->N;
+    memcpy(c->psi, psi, bytes);
+    c->slot->op = QCS_OP_HDOT;
+    const int rc = call(c);
+    if (rc == QCC_OK) memcpy(psi, c->psi, bytes);
     return rc;
 }

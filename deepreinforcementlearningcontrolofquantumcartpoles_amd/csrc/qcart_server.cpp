@@ -32,6 +32,10 @@
 #include "../../include/qcart.h"
 #include "qcart_shm.h"
 
+namespace qcart {
+void set_global_error(const std::string& m);   // qcart_api.cpp: what qc_last_error(NULL) returns
+}
+
 namespace {
 
 int futex_wait(uint32_t* addr, uint32_t val, long timeout_ns) {
@@ -89,6 +93,8 @@ struct qc_server {
     double *q10 = nullptr, *d_q10 = nullptr, *xm10 = nullptr, *d_xm10 = nullptr; // [10][P]
     int32_t *fs1 = nullptr, *d_fs1 = nullptr, *fb10 = nullptr, *d_fb10 = nullptr; // [P]
     double *xe = nullptr, *d_xe = nullptr;           // [P]
+    double *hp = nullptr, *d_hp = nullptr;           // [P][2N] Hamiltonian_dot_psi rows (the op writes every row of
+                                                     // its buffer: never the clients' own rows, nor the step buffer)
     double *obs = nullptr, *d_obs = nullptr;         // [P][n_obs]
     // the clients' state rows registered with HIP (device-mapped): the kernels step them in place, no copy in or out
     // (QCART_SERVER_INPLACE=0, or a failed registration: copies through `psi`)
@@ -146,7 +152,7 @@ int slot_of(qc_server* s, double force, int& slot) {
 void free_server(qc_server* s) {
     if (s->h) qc_destroy(s->h);
     void* hb[] = {s->psi, s->act, s->st1, s->st10, s->seeds, s->mask, s->q1, s->xm1, s->q10, s->xm10, s->fs1, s->fb10,
-                  s->xe, s->obs, s->has_pre, s->gen, s->pf};
+                  s->xe, s->obs, s->has_pre, s->gen, s->pf, s->hp};
     for (void* b : hb)
         if (b) (void)hipHostFree(b);
     if (s->d_pre) (void)hipFree(s->d_pre);
@@ -168,7 +174,7 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
     const int P = s->P, N = s->N;
     struct Req { int op, n; uint32_t seed; double dt, force, gamma; };
     std::vector<Req> rq(P);
-    bool any_seed = false, any_x = false, any_obs = false;
+    bool any_seed = false, any_x = false, any_obs = false, any_h = false;
     std::vector<int> g1, g10;   // step groups
     for (int e : pend) {
         qcs_slot& sl = s->slots[e];
@@ -181,6 +187,16 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
             s->mask[e] = 1;
             s->pre_ok[e] = 0;   // a drawn pair belongs to the old stream
             any_seed = true;
+            continue;
+        }
+        if (r.op == QCS_OP_HDOT) {
+            if (!s->hp) {   // (grid modules have no Hamiltonian_dot_psi)
+                sl.status = QC_EINVAL;
+                std::snprintf(sl.err, sizeof(sl.err), "Hamiltonian_dot_psi is a Fock-module function");
+                continue;
+            }
+            std::memcpy(s->hp + (size_t)e * 2 * N, s->spsi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
+            any_h = true;
             continue;
         }
         if (!s->inplace) std::memcpy(s->psi + (size_t)e * 2 * N, s->spsi + (size_t)e * 2 * N, sizeof(double) * 2 * N);
@@ -263,9 +279,13 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
         const int rc = qc_x_expectation(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_xe);
         if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op == QCS_OP_X_EXPECT) es.push_back(e); err_all(es, rc); }
     }
+    if (any_h) {
+        const int rc = qc_hamiltonian_dot_psi(s->h, s->d_hp);
+        if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op == QCS_OP_HDOT) es.push_back(e); err_all(es, rc); }
+    }
     if (any_obs) {
         const int rc = qc_moments(s->h, s->inplace ? s->d_spsi : s->d_psi, s->d_obs);
-        if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op >= QCS_OP_MOMENTS) es.push_back(e); err_all(es, rc); }
+        if (rc) { std::vector<int> es; for (int e : pend) if (rq[e].op == QCS_OP_MOMENTS || rq[e].op == QCS_OP_FOCK_OBS) es.push_back(e); err_all(es, rc); }
     }
     const double t_l = now_us();
     hipError_t e = hipSuccess;
@@ -299,6 +319,8 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
                 }
             } else if (r.op == QCS_OP_X_EXPECT) {
                 sl.value = s->xe[e];
+            } else if (r.op == QCS_OP_HDOT) {
+                std::memcpy(s->spsi + (size_t)e * 2 * N, s->hp + (size_t)e * 2 * N, sizeof(double) * 2 * N);
             } else if (r.op == QCS_OP_MOMENTS || r.op == QCS_OP_FOCK_OBS) {
                 std::memcpy(s->sobs + (size_t)e * QCS_MAX_OBS, s->obs + (size_t)e * s->n_obs, sizeof(double) * s->n_obs);
             }
@@ -339,12 +361,28 @@ void reap_dead_clients(qc_server* s) {
         const int32_t pid = __atomic_load_n(&sl.pid, __ATOMIC_ACQUIRE);
         if (!ld_acq(&sl.owner) || pid <= 0) continue;
         if (kill(pid, 0) == 0 || errno != ESRCH) continue;
+        // a pending request is published as dropped, never as served (its state row and results were not written)
+        sl.status = QCS_EDROPPED;
+        std::snprintf(sl.err, sizeof(sl.err), "request dropped: client process %d exited", (int)pid);
         s->served[e] = __atomic_load_n(&sl.req, __ATOMIC_ACQUIRE);
         __atomic_store_n(&sl.done, s->served[e], __ATOMIC_RELEASE);
         __atomic_store_n(&sl.pid, 0, __ATOMIC_RELAXED);
         __atomic_sub_fetch(&s->hdr->n_clients, 1u, __ATOMIC_SEQ_CST);
         __atomic_store_n(&sl.owner, 0u, __ATOMIC_RELEASE);
     }
+}
+
+// an existing step-server object whose server is gone: it stopped (alive 0) or its process no longer exists in this
+// PID namespace. Anything else (a live server, another program's object, one from another namespace) is kept.
+bool stale_object(const char* name) {
+    const int fd = shm_open(name, O_RDONLY, 0);
+    if (fd < 0) return false;
+    qcs_header h{};
+    const bool got = pread(fd, &h, sizeof(h), 0) == (ssize_t)sizeof(h);
+    close(fd);
+    if (!got || h.magic != QCS_MAGIC || h.version != QCS_VERSION || h.pid_ns != qcs_pid_ns()) return false;
+    if (!__atomic_load_n(&h.alive, __ATOMIC_RELAXED)) return true;
+    return h.server_pid > 0 && kill(h.server_pid, 0) != 0 && errno == ESRCH;
 }
 
 void scan(qc_server* s, std::vector<int>& pend, int& owned) {
@@ -380,7 +418,14 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     s->cur_dt = p->dt;
     s->cur_gamma = p->gamma;
     const int P = s->P, N = s->N;
-    auto bail = [&](int code, const std::string& m) { s->err = m; free_server(s); delete s; return code; };
+    // (the message also goes to qc_last_error(NULL): the caller has no server handle to ask)
+    auto bail = [&](int code, const std::string& m) {
+        s->err = m;
+        qcart::set_global_error(m);
+        free_server(s);
+        delete s;
+        return code;
+    };
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(QC_EHIP, "hipStreamCreate failed");
     if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess)
@@ -396,7 +441,8 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
         host_alloc(&s->q10, &s->d_q10, (size_t)10 * P) || host_alloc(&s->xm10, &s->d_xm10, (size_t)10 * P) ||
         host_alloc(&s->fs1, &s->d_fs1, P) || host_alloc(&s->fb10, &s->d_fb10, P) || host_alloc(&s->xe, &s->d_xe, P) ||
         host_alloc(&s->obs, &s->d_obs, (size_t)P * (s->n_obs > 0 ? s->n_obs : 1)) ||
-        host_alloc(&s->has_pre, &s->d_has_pre, P) || host_alloc(&s->gen, &s->d_gen, P) || host_alloc(&s->pf, &s->d_pf, P))
+        host_alloc(&s->has_pre, &s->d_has_pre, P) || host_alloc(&s->gen, &s->d_gen, P) || host_alloc(&s->pf, &s->d_pf, P) ||
+        (p->family <= 1 && host_alloc(&s->hp, &s->d_hp, (size_t)P * 2 * N)))
         return bail(QC_ENOMEM, "pinned host buffers");
     {
         const char* m = std::getenv("QCART_SERVER_PREFETCH");
@@ -415,6 +461,11 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     const size_t obs_off = round_up(psi_off + sizeof(double) * 2 * N * P, 4096);
     const size_t total = round_up(obs_off + sizeof(double) * QCS_MAX_OBS * P, 4096);
     s->fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (s->fd < 0 && errno == EEXIST && stale_object(name)) {
+        // left behind by a server that died without qc_server_destroy: replaced
+        shm_unlink(name);
+        s->fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    }
     if (s->fd < 0) return bail(QC_EINVAL, std::string("shm_open(") + name + "): " + strerror(errno));
     s->name = name;
     if (ftruncate(s->fd, (off_t)total) != 0) return bail(QC_ENOMEM, "ftruncate");
@@ -465,6 +516,8 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     H->mass = p->mass;
     H->f_max = p->f_max;
     H->n_actions = p->n_actions;
+    H->server_pid = (int32_t)getpid();
+    H->pid_ns = qcs_pid_ns();
     s->served.assign(P, 0u);
     s->pre_ok.assign(P, 0);
     __atomic_store_n(&H->alive, 1u, __ATOMIC_SEQ_CST);

@@ -16,9 +16,10 @@
 #define QCART_SHM_H
 
 #include <stdint.h>
+#include <sys/stat.h>
 
 #define QCS_MAGIC 0x56534351u /* "QCSV" */
-#define QCS_VERSION 1u
+#define QCS_VERSION 2u
 #define QCS_MAX_OBS 64        /* >= the largest n_obs ((2+9+1)*9/2 = 54 grid moments) */
 
 /* request operations (the reference module's functions, IHO/simulation_i.cpp:618-631, QO/simulation_quart.cpp:656-668) */
@@ -27,8 +28,11 @@ enum qcs_op {
     QCS_OP_SET_SEED = 2,   /* set_seed(seed): the env's MT19937 stream restarts */
     QCS_OP_X_EXPECT = 3,   /* x_expectation(state) */
     QCS_OP_MOMENTS = 4,    /* get_moments(state, data) (grid) */
-    QCS_OP_FOCK_OBS = 5    /* the Fock 'xp' 5-vector (IHO/main_parallel.py:129-131) */
+    QCS_OP_FOCK_OBS = 5,   /* the Fock 'xp' 5-vector (IHO/main_parallel.py:129-131) */
+    QCS_OP_HDOT = 6        /* Hamiltonian_dot_psi(state): the row <- H row (Fock; IHO/simulation_i.cpp:585-601) */
 };
+
+#define QCS_EDROPPED (-100)   /* a slot status: the server released the slot without serving the request */
 
 typedef struct qcs_header {
     uint32_t magic, version;
@@ -38,13 +42,16 @@ typedef struct qcs_header {
     uint32_t kick;           /* incremented (and futex-woken) by a client whose request finds the server asleep */
     uint32_t server_sleeping;
     uint32_t n_clients;      /* slots currently owned */
-    uint32_t pad0;
+    int32_t server_pid;      /* the serving process: a client whose server died without clearing `alive` (killed,
+                                aborted on a GPU fault) sees kill(server_pid, 0) fail with ESRCH */
     uint64_t slot_off, psi_off, obs_off, total_bytes;
     /* the module's compiled parameters (check_settings) */
     int32_t n_max, moment_order;
     double omega, x_max, grid_size, lambda_, mass, f_max;
     int32_t n_actions, pad1;
     uint64_t ticks, calls;   /* served ticks / requests (statistics, server-written) */
+    uint64_t pid_ns;         /* inode of the server's PID namespace (/proc/self/ns/pid): pids are compared only
+                                inside one namespace, so clients from another are refused */
 } qcs_header;
 
 typedef struct qcs_slot {
@@ -56,12 +63,18 @@ typedef struct qcs_slot {
     int32_t op, n;
     uint32_t seed;
     double dt, force, gamma;
-    int32_t status;          /* 0 ok, < 0 a qc_status code */
+    int32_t status;          /* 0 ok, < 0 a qc_status code (QCS_EDROPPED: the request was dropped unserved) */
     int32_t fail;            /* step: Fail */
     double q, xmean;         /* step: the last step's q and x_mean */
     double value;            /* x_expectation */
     char err[96];
     uint8_t pad[32];
 } qcs_slot;
+
+/* inode of this process's PID namespace (0 if /proc is unavailable) */
+static inline uint64_t qcs_pid_ns(void) {
+    struct stat st;
+    return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0u;
+}
 
 #endif

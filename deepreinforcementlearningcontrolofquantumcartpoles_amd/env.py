@@ -239,10 +239,7 @@ class BatchedEnv:
         fam = self.ph.family
         pend = self._pending
         reset_now = pend.clone().view(torch.bool)
-        if fam == cfg.IHO:
-            self.st.reset(self.psi, 0, mask=pend)
-        else:
-            self.st.reset(self.psi, 2, mask=pend, arg0=0.0, arg1=0.0, arg2=1.0)
+        self._reset_states(reset_now)   # the immediate mode's reset (reset_kind included), masked
         acts = torch.where(reset_now, torch.full_like(actions, self.half), actions)
         out = self.st.step(self.psi, acts, self.ci, want_fail=True, want_obs=True, want_term=(fam == cfg.IQO))
         B, n = self.B, self.st.n_obs

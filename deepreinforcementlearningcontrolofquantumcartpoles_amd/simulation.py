@@ -216,6 +216,7 @@ def _client_lib():
         L.qcc_set_seed.argtypes = [vp, ctypes.c_uint32]
         L.qcc_x_expectation.argtypes = [vp, vp, P(d)]
         L.qcc_moments.argtypes = [vp, vp, vp]
+        L.qcc_hamiltonian_dot_psi.argtypes = [vp, vp]
         _CLIENT_LIB = L
     return _CLIENT_LIB
 
@@ -291,6 +292,16 @@ class _ServedSimulation:
         st = np.ascontiguousarray(state)
         self._check(self._L.qcc_x_expectation(self._c, st.ctypes.data, ctypes.byref(self._v)))
         return self._v.value
+
+    # Hamiltonian_dot_psi(state) (Fock modules, IHO/simulation_i.cpp:585-601): served on the server's batch
+    def Hamiltonian_dot_psi(self, state):
+        _check_state(state, self.N)
+        if not state.flags.c_contiguous or not state.flags.writeable:
+            raise ValueError("The input array is not a writeable contiguous array")
+        self._check(self._L.qcc_hamiltonian_dot_psi(self._c, state.ctypes.data))
+        return 0.0
+
+    solve_ab = _Simulation.solve_ab
 
     def get_moments(self, state, data):
         _check_state(state, self.N)
@@ -403,8 +414,8 @@ def load(family: int | str = cfg.IHO, device: int = 0, noise: str = "mt19937", s
             setattr(mod, name, getattr(sim, name))
         if not phys.fock:
             mod.get_moments = sim.get_moments
-        elif server is None:
-            # the Fock modules' method tables (IHO/simulation_i.cpp:618-631, HO/simulation.cpp:599-612)
+        else:
+            # the Fock modules' method tables (IHO/simulation_i.cpp:618-631, HO/simulation.cpp:599-612), served too
             mod.Hamiltonian_dot_psi = sim.Hamiltonian_dot_psi
             mod.solve_ab = sim.solve_ab
         mod._impl = sim

@@ -61,6 +61,9 @@ int qcc_x_expectation(qcc* c, const double* psi, double* out);
 /* get_moments(state, data) (grid: QO/simulation_quart.cpp:326-388, n_obs values) or the Fock 'xp' 5-vector
  * (IHO/main_parallel.py:129-131) */
 int qcc_moments(qcc* c, const double* psi, double* out);
+/* Hamiltonian_dot_psi(state) (Fock modules; IHO/simulation_i.cpp:585-601, HO/simulation.cpp:566-582): psi <- H psi
+ * in place with the force-free Hamiltonian */
+int qcc_hamiltonian_dot_psi(qcc* c, double* psi);
 
 #ifdef __cplusplus
 }

@@ -234,9 +234,9 @@ def test_out_of_range_actions_raise_at_the_next_check():
 
 
 
-def _episodes_per_env(mode, ph, B, calls, policy):
+def _episodes_per_env(mode, ph, B, calls, policy, reset_kind="reference"):
     """Each env's finished episodes (return, length, first-interval flag) in its own order, and the ring."""
-    env = BatchedEnv(ph, B, 0, seed=5, reset=mode)
+    env = BatchedEnv(ph, B, 0, seed=5, reset=mode, reset_kind=reset_kind)
     env.reset()
     per = [[] for _ in range(B)]
     for _ in range(calls):
@@ -253,8 +253,8 @@ def _episodes_per_env(mode, ph, B, calls, policy):
     return per, env
 
 
-@pytest.mark.parametrize("fam", [cfg.IHO, cfg.IQO])
-def test_deferred_reset_keeps_every_envs_episodes(fam):
+@pytest.mark.parametrize("fam, kind", [(cfg.IHO, "reference"), (cfg.IQO, "reference"), (cfg.IHO, "synthetic")])
+def test_deferred_reset_keeps_every_envs_episodes(fam, kind):
     """reset='deferred' (a finished env takes its reset interval in the next call, inside the same step launch,
     bookkeeping on the device by qc_env_tail, no host sync): every env's own episode sequence — returns and
     lengths — is bitwise the immediate mode's (per-env noise keyed by the env's own step count, a policy of the
@@ -264,8 +264,8 @@ def test_deferred_reset_keeps_every_envs_episodes(fam):
 
     def policy(obs):   # a deterministic bad controller: pushes the pole the way it leans (episodes end)
         return torch.where(obs[:, 0] > 0, 20, 0).to(torch.int32)
-    imm, _ = _episodes_per_env("immediate", ph, B, 40, policy)
-    dfr, env = _episodes_per_env("deferred", ph, B, 48, policy)
+    imm, _ = _episodes_per_env("immediate", ph, B, 40, policy, kind)
+    dfr, env = _episodes_per_env("deferred", ph, B, 48, policy, kind)
     n = 0
     for e in range(B):
         k = min(len(imm[e]), len(dfr[e]))

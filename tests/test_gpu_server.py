@@ -244,3 +244,90 @@ def test_killed_client_slot_is_released():
     finally:
         srv.close()
 
+
+
+@pytest.mark.parametrize("family, n_max", [(cfg.IHO, 63), (cfg.HO, 40)])
+def test_served_hamiltonian_dot_psi_equals_the_plain_dropin(family, n_max):
+    """The Fock modules' Hamiltonian_dot_psi (IHO/simulation_i.cpp:585-601) through the server, while another client
+    steps in the same ticks: bitwise the plain drop-in's H psi, and the stepping client's state untouched by it;
+    solve_ab refused as by the plain module."""
+    rng = np.random.default_rng(7)
+    st0 = rng.standard_normal(n_max + 1) + 1j * rng.standard_normal(n_max + 1)
+    plain = S.load(family, n_max=n_max)
+    want = st0.copy()
+    assert plain.Hamiltonian_dot_psi(want) == 0.0
+    plain.set_seed(5)
+    ws = np.zeros(n_max + 1, np.complex128)
+    ws[0] = 1
+    for _ in range(50):
+        plain.step(ws, 1 / 1440, 0.8, pi)
+    name = _name()
+    srv = S.StepServer(family, max_clients=2, name=name, n_max=n_max).start()
+    try:
+        ph = cfg.DEFAULTS[family].with_(n_max=n_max)
+        a, b = S._ServedSimulation(ph, name), S._ServedSimulation(ph, name)
+        b.set_seed(5)
+        gs = np.zeros(n_max + 1, np.complex128)
+        gs[0] = 1
+        got = st0.copy()
+
+        def stepper():
+            for _ in range(50):
+                b.step(gs, 1 / 1440, 0.8, pi)
+        t = threading.Thread(target=stepper)
+        t.start()
+        for _ in range(20):
+            got = st0.copy()
+            assert a.Hamiltonian_dot_psi(got) == 0.0
+        t.join()
+        assert np.array_equal(got, want)
+        assert np.array_equal(gs, ws)
+        with pytest.raises(NotImplementedError):
+            a.solve_ab(got)
+        mod = S.load(family, server=name, n_max=n_max)
+        assert hasattr(mod, "Hamiltonian_dot_psi") and hasattr(mod, "solve_ab")
+        mod._impl.close()
+        a.close()
+        b.close()
+    finally:
+        srv.close()
+
+
+def test_server_name_collision_and_stale_objects():
+    """A second server under a live server's name fails with the shm error in its message (qc_last_error(NULL));
+    an object left by a server that died without qc_server_destroy (alive still 1, its pid gone) is replaced."""
+    import subprocess
+    import sys
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib
+    from tests.test_server_protocol import Header
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=1, name=name, n_max=63)
+    try:
+        with pytest.raises(_lib.QCartError, match="File exists"):
+            S.StepServer(cfg.IHO, max_clients=1, name=name, n_max=63)
+    finally:
+        srv.close()
+    # a dead server's object
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    name2 = _name()
+    with open("/dev/shm" + name2, "wb") as f:
+        h = Header()
+        h.magic, h.version, h.alive, h.server_pid = 0x56534351, 2, 1, dead.pid
+        h.pid_ns = os.stat("/proc/self/ns/pid").st_ino
+        f.write(bytes(h))
+        f.truncate(8192)
+    try:
+        with pytest.raises(RuntimeError, match="no live step server"):
+            S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name2)
+        srv2 = S.StepServer(cfg.IHO, max_clients=1, name=name2, n_max=63).start()
+        m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name2)
+        st = np.zeros(64, np.complex128)
+        st[0] = 1
+        q, xm, fail = m.step(st, 1 / 1440, 0.0, 2 * pi)
+        assert fail == 0 and np.isfinite(q)
+        m.close()
+        srv2.close()
+    finally:
+        if os.path.exists("/dev/shm" + name2):
+            os.unlink("/dev/shm" + name2)

@@ -25,9 +25,10 @@ u32, i32, u64, d = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_do
 class Header(ctypes.Structure):
     _fields_ = [("magic", u32), ("version", u32), ("max_clients", i32), ("N", i32), ("n_obs", i32), ("family", i32),
                 ("alive", u32), ("tick", u32), ("kick", u32), ("server_sleeping", u32), ("n_clients", u32),
-                ("pad0", u32), ("slot_off", u64), ("psi_off", u64), ("obs_off", u64), ("total_bytes", u64),
+                ("server_pid", i32), ("slot_off", u64), ("psi_off", u64), ("obs_off", u64), ("total_bytes", u64),
                 ("n_max", i32), ("moment_order", i32), ("omega", d), ("x_max", d), ("grid_size", d), ("lambda_", d),
-                ("mass", d), ("f_max", d), ("n_actions", i32), ("pad1", i32), ("ticks", u64), ("calls", u64)]
+                ("mass", d), ("f_max", d), ("n_actions", i32), ("pad1", i32), ("ticks", u64), ("calls", u64),
+                ("pid_ns", u64)]
 
 
 class Slot(ctypes.Structure):
@@ -36,7 +37,7 @@ class Slot(ctypes.Structure):
                 ("xmean", d), ("value", d), ("err", ctypes.c_char * 96), ("pad", ctypes.c_uint8 * 32)]
 
 
-OP_STEP, OP_SET_SEED, OP_X, OP_MOM, OP_FOCK = 1, 2, 3, 4, 5
+OP_STEP, OP_SET_SEED, OP_X, OP_MOM, OP_FOCK, OP_HDOT = 1, 2, 3, 4, 5, 6
 MAX_OBS = 64
 
 
@@ -63,10 +64,12 @@ def test_layout_mirror_matches_the_c_header(tmp_path):
 class MockServer:
     """qcart_server.cpp's side of the protocol in Python: STEP negates the state and reports q = 1.5 n,
     x_mean = force, Fail = n == 10; SET_SEED stores the seed in `value`; X_EXPECT returns the sum of Re(psi);
-    MOMENTS fills the obs row with 0, 1, 2, ..."""
+    MOMENTS fills the obs row with 0, 1, 2, ...; HDOT doubles the row. serve_ops: the ops it answers (others stay
+    pending forever: a server that hangs on them)."""
 
-    def __init__(self, name, P=3, N=8, n_obs=5):
+    def __init__(self, name, P=3, N=8, n_obs=5, serve_ops=None):
         self.name, self.P, self.N, self.n_obs = name, P, N, n_obs
+        self.serve_ops = serve_ops
         rnd = lambda v: (v + 4095) // 4096 * 4096   # noqa: E731
         self.slot_off = rnd(ctypes.sizeof(Header))
         self.psi_off = rnd(self.slot_off + ctypes.sizeof(Slot) * P)
@@ -82,7 +85,8 @@ class MockServer:
         self.psi = np.frombuffer(self.mm, np.complex128, N * P, self.psi_off).reshape(P, N)
         self.obs = np.frombuffer(self.mm, np.float64, MAX_OBS * P, self.obs_off).reshape(P, MAX_OBS)
         h = self.hdr
-        h.magic, h.version, h.max_clients, h.N, h.n_obs, h.family = 0x56534351, 1, P, N, n_obs, 1
+        h.magic, h.version, h.max_clients, h.N, h.n_obs, h.family = 0x56534351, 2, P, N, n_obs, 1
+        h.server_pid, h.pid_ns = os.getpid(), os.stat("/proc/self/ns/pid").st_ino
         h.slot_off, h.psi_off, h.obs_off, h.total_bytes = self.slot_off, self.psi_off, self.obs_off, self.total
         h.n_max, h.omega = N - 1, 3.14159
         h.alive = 1
@@ -99,6 +103,8 @@ class MockServer:
                 s = self.slots[e]
                 if not s.owner or s.req == self.served[e]:
                     continue
+                if self.serve_ops is not None and s.op not in self.serve_ops:
+                    continue
                 any_ = True
                 if s.op == OP_STEP:
                     self.psi[e] *= -1
@@ -107,6 +113,8 @@ class MockServer:
                     s.value = float(s.seed)
                 elif s.op == OP_X:
                     s.value = float(self.psi[e].real.sum())
+                elif s.op == OP_HDOT:
+                    self.psi[e] *= 2
                 else:
                     self.obs[e, :self.n_obs] = np.arange(self.n_obs)
                 s.status = 0
@@ -158,6 +166,10 @@ def test_client_calls_through_the_protocol():
         assert (q, xm, fail) == (1.5, 0.8, 0) and np.array_equal(state, -(np.arange(8) + 1j))
         q, xm, fail = b.simulate_10_steps(state, 1 / 1440, -1.6, 6.28)
         assert (q, xm, fail) == (15.0, -1.6, 1) and np.array_equal(state, np.arange(8) + 1j)
+        assert a.Hamiltonian_dot_psi(state) == 0.0 and np.array_equal(state, 2 * (np.arange(8) + 1j))
+        state /= 2
+        with pytest.raises(NotImplementedError):
+            a.solve_ab(state)
         a.set_seed(2 ** 32 + 77)                        # the int's low 32 bits, as the reference's MKL_UINT
         assert srv.slots[0].value == 77.0
         assert a.x_expectation(state) == float(np.arange(8).sum())
@@ -186,3 +198,60 @@ def test_client_calls_through_the_protocol():
             S._ServedSimulation(ph.with_(n_max=15), srv.name)
     finally:
         srv.close()
+
+
+_DYING = """
+import sys, time
+sys.path.insert(0, {root!r})
+from tests.test_server_protocol import MockServer, OP_SET_SEED
+srv = MockServer({name!r}, P=2, N=8, serve_ops={{OP_SET_SEED}})   # answers set_seed (qcc_open's), never a step
+print("ready", flush=True)
+time.sleep(600)
+"""
+
+
+def test_client_detects_a_killed_server():
+    """A server killed without clearing `alive` (SIGKILL, a GPU-fault abort): a client waiting on it fails within a
+    second (the 20 ms liveness check reads the server's pid), qcc_close returns, and the object it left behind is
+    refused by the next qcc_open."""
+    import signal
+    import sys
+    S = _client_module()
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    name = f"/qcart_dying_{os.getpid()}"
+    proc = subprocess.Popen([sys.executable, "-c", _DYING.format(root=ROOT, name=name)], cwd=ROOT,
+                            stdout=subprocess.PIPE, text=True)
+    try:
+        assert proc.stdout.readline().strip() == "ready"
+        ph = cfg.DEFAULTS[cfg.IHO].with_(n_max=7, omega=3.14159)
+        a = S._ServedSimulation(ph, name)
+        out = {}
+
+        def call():
+            t0 = time.monotonic()
+            try:
+                a.step(np.zeros(8, np.complex128), 1 / 1440, 0.0, 6.28)
+            except RuntimeError as e:
+                out["err"] = str(e)
+            out["dt"] = time.monotonic() - t0
+        th = threading.Thread(target=call)
+        th.start()
+        time.sleep(0.3)
+        assert th.is_alive()                      # the step is pending: the server never answers it
+        t_kill = time.monotonic()
+        proc.send_signal(signal.SIGKILL)
+        proc.wait()
+        th.join(timeout=10)
+        assert not th.is_alive()
+        assert "exited" in out["err"] and time.monotonic() - t_kill < 2.0, out
+        t0 = time.monotonic()
+        a.close()                                 # the pending request does not hold the close
+        assert time.monotonic() - t0 < 1.0
+        with pytest.raises(RuntimeError, match="no live step server"):
+            S._ServedSimulation(ph, name)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+        if os.path.exists("/dev/shm" + name):
+            os.unlink("/dev/shm" + name)

@@ -99,4 +99,7 @@ BENCH_CONFIGS = {
     "C4": dict(physics=DEFAULTS[IQO].with_(x_max=12.8, grid_size=0.05), batch=65536),
     "C5": dict(physics=DEFAULTS[IHO].with_(n_max=2047, precision=1), batch=262144),
     "metric": dict(physics=DEFAULTS[IHO].with_(n_max=511), batch=65536),
+    # diagnostic (not a BASELINE config): C5's fp32 IHO kernel at N = 1024, R = 16 rows per lane, two waves per SIMD —
+    # the per-wave side of C5's cost split (profiles/r06_C5r16_*)
+    "C5r16": dict(physics=DEFAULTS[IHO].with_(n_max=1023, precision=1), batch=32768),
 }

@@ -284,11 +284,11 @@ def test_served_hamiltonian_dot_psi_equals_the_plain_dropin(family, n_max):
         assert np.array_equal(gs, ws)
         with pytest.raises(NotImplementedError):
             a.solve_ab(got)
-        mod = S.load(family, server=name, n_max=n_max)
-        assert hasattr(mod, "Hamiltonian_dot_psi") and hasattr(mod, "solve_ab")
-        mod._impl.close()
         a.close()
         b.close()
+        mod = S.load(family, server=name, n_max=n_max)   # the module table of a served Fock module
+        assert hasattr(mod, "Hamiltonian_dot_psi") and hasattr(mod, "solve_ab")
+        mod._impl.close()
     finally:
         srv.close()
 

@@ -17,6 +17,16 @@
 #ifndef QCART_W8_MAX_RG
 #define QCART_W8_MAX_RG 9
 #endif
+// grid step kernels up to R = 9: the host-folded step constants of the Fock kernels (HC; round 6, alternating
+// same-call pairs: C4 9.09 -> 8.91 ms; C3's R = 17 kernel with them, 150.2 -> 149.0 ms, computed wrong values, k_step
+// comment). QCART_GRID_KAR: the per-step kernarg re-read for R = 17 too (A/B knob; with HC: C3's spilled SGPRs
+// 260 -> 109, 151.2 vs 149.8 ms against the shipped kernel)
+#ifndef QCART_GRID_HC
+#define QCART_GRID_HC 1
+#endif
+#ifndef QCART_GRID_KAR
+#define QCART_GRID_KAR 0
+#endif
 // band solve: the fp32 Fock kernels' whole-wave Kogge-Stone (no row carry) for up to this many kept levels (0: off;
 // 3: C5 -1.6 %)
 #ifndef QCART_WKS_F32

@@ -1472,11 +1472,13 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         xbar = (RT)(a.w * s[0]);                                  // x_expct (IHO:197-203, QO:230-236)
         if (win_on && 1.0 - s[1] * a.h > 0.5) term = 0;
     }
-    // uniform step constants: host-folded kernel arguments for the Fock kernels, where device-side they were
-    // VGPR values the register allocator spilled (metric: 35 spilled registers -> 0, -1.7 %); the grid kernels
-    // keep the device-side forms (their schedule measured 2-3 % faster that way). Same values. (Read in the
-    // step loop, below.)
-    constexpr bool HC = FAM != 2;
+    // uniform step constants: host-folded kernel arguments, where device-side they were VGPR values the register
+    // allocator spilled (metric: 35 spilled registers -> 0, -1.7 %). The grid kernels up to R = 9 too since round 6
+    // (QCART_GRID_HC: C4 9.09 -> 8.91 ms in alternating same-call pairs). Not the R = 17 kernel (C3): with them its
+    // MODE 4 instantiation (260 spilled SGPRs at the 106 limit) stepped wrongly from the first step — NaN in
+    // test_stepper_tracks_mkl_reference_trajectory_v3[qo1025] while the same source's MODE 0 kernel tracked the
+    // fixture: the round-4 wrong-spill-lane class. Same values. (Read in the step loop, below.)
+    constexpr bool HC = FAM != 2 || (QCART_GRID_HC && R < 17);
     const uint32_t genv = (uint32_t)(a.env_offset + env);
     // the noise of the next 64 steps (lane j: step k + j): in the wave's LDS buffer (NZL) or in two registers
     constexpr bool NZL = MODE >= 1 && sizeof(RT) == 8 && QCART_NZ_LDS;
@@ -1486,7 +1488,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the env's own noise position: it advances by the steps this env takes, so an env's stream never
     // depends on which other envs of the handle step in the same call (auto-reset, sharding)
     const uint64_t ctr0 = a.ctr[env];
-    constexpr bool KAR = !(FAM == 2 && R >= 17);
+    constexpr bool KAR = !(FAM == 2 && R >= 17) || QCART_GRID_KAR;
     // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
     // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)

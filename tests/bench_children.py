@@ -5,6 +5,8 @@ run one after another (python -m tests.bench_children <outdir>); tests/test_gpu_
   share2  `bench.py --gpus 2` through bench.py's own launcher with QCART_BENCH_SHARE_DEVICE=1: both ranks on
           device 0, gloo carrying the collectives (the N-rank path rehearsed on a one-GPU lease)
   whole1  a plain one-rank run of the two ranks' envs together, for the shard-digest comparison
+  trun2   the driver's own launch, `python -m torch.distributed.run --nproc-per-node 2 ... bench.py --gpus 2`, with
+          QCART_BENCH_SHARE_DEVICE=1 (both ranks on device 0, gloo)
 
 Each run is a process group of its own, bounded at 300 s (then killed whole, rc 124); after the first failure
 nothing more is started; SIGTERM kills the running group and ends the runner. Writes <name>.log (stdout +
@@ -34,6 +36,12 @@ def runs():
     yield "share2", dict(base, QCART_BENCH_SHARE_DEVICE="1"), \
         [bench, "--gpus", "2", "--batch", str(BATCH), "--digest-envs", str(BATCH), "--launch-timeout", "240"] + COMMON
     yield "whole1", base, [bench, "--gpus", "1", "--batch", str(2 * BATCH), "--digest-envs", str(BATCH)] + COMMON
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port2 = sk.getsockname()[1]
+    yield "trun2", dict(base, QCART_BENCH_SHARE_DEVICE="1"), \
+        ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+         "--master-port", str(port2), bench, "--gpus", "2", "--batch", str(BATCH), "--digest-envs", str(BATCH)] + COMMON
 
 
 LIMIT_S = 300

@@ -61,3 +61,21 @@ def test_launch_deadline_kills_hung_ranks():
                env={"QCART_BENCH_HANG_RANK": "1", "QCART_DIST_TIMEOUT_S": "120"})
     assert out.returncode == 124 and time.monotonic() - t0 < 30, out.stderr[-2000:]
     assert "all ranks killed" in out.stderr
+
+
+def test_torchrun_launch_dry_run():
+    """The driver's launch (python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 ...
+    bench.py --gpus 2): the ranks take RANK / WORLD_SIZE from torchrun and join one group."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--dry-run"], env=e, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert lines == [{"dry_run": True, "n_gpus": 2, "world_size_seen": 2}]

@@ -10,7 +10,8 @@ another:
   share2  `bench.py --gpus 2` through bench.py's own launcher with QCART_BENCH_SHARE_DEVICE=1: two ranks on
           device 0, gloo carrying the same collectives — the path the driver's 8-GPU run takes, on one GPU;
   whole1  one plain rank stepping both ranks' envs (2B) — rank r's shard must equal envs [rB, (r+1)B) of it bit
-          for bit (inputs, psi0 and noise are keyed by the global env id).
+          for bit (inputs, psi0 and noise are keyed by the global env id);
+  trun2   the driver's launch (torch.distributed.run, 2 processes) on one device.
 These tests read the runs' JSON lines."""
 import json
 import os
@@ -80,3 +81,14 @@ def test_rank_shards_equal_the_one_rank_run_bitwise(request):
     assert len(two) == 2 and len(one) == 2
     assert two == one                               # rank r's final psi == envs [rB, (r+1)B) of the 2B run
     assert two[0] != two[1]
+
+
+@pytest.mark.timeout(1000)
+def test_torchrun_launch_on_one_device(request):
+    """The driver's own N-rank launch (python -m torch.distributed.run --nproc-per-node 2 ... bench.py --gpus 2): world
+    2, one JSON line from rank 0, the same shard digests as bench.py's own launcher."""
+    outdir = _wait(request)
+    res = _result(outdir, "trun2")
+    assert res["n_gpus"] == 2 and res["config"]["world_size_seen"] == 2
+    assert res["config"]["rccl"]["gathered_envs"] == 2 * BATCH
+    assert res["psi_digests"] == _result(outdir, "whole1")["psi_digests"]

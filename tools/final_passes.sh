@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 echo "pytest rc=$rc"; tail -1 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 TAG=$TAG bash tools/run_table.sh || exit $?
-bash tools/sq_configs.sh "$TAG" C5 C3 C4 metric || exit $?
+bash tools/sq_configs.sh "$TAG" C5 C3 C4 metric C2 || exit $?
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1; rc=$?
 echo "default bench rc=$rc"; grep '^{' gpurun_out/bench_default.log | tail -1; [ $rc -eq 0 ] || exit $rc
 # the end-to-end actor loop (both reset modes) and the drop-in under the reference's process model

@@ -199,11 +199,12 @@ static int call(qcc* c) {
         syscall(SYS_futex, &h->kick, FUTEX_WAKE, 1, NULL, NULL, 0);
     }
     /* a short spin (a tick takes tens of microseconds), then sleep on the tick word. Adaptive (no QCC_SPIN_US):
-     * 150 us while every attached client has a CPU of its own, 20 us once they outnumber the usable CPUs — the
-     * reference's 30-40 actors on a 16-CPU share: spinning clients would take the CPU from the ones whose tick
-     * has completed (P = 32: 4.6e5 vs 3.6e5 step calls/s, P = 40: 5.3e5 vs 3.2e5) */
+     * 150 us while every attached client has a CPU of its own (P = 16 at n_max = 180: 4.9e5 step calls/s against
+     * 3.5e5 with 20 us), none once they outnumber the usable CPUs — the reference's 30-40 actors on a 16-CPU share,
+     * where a polling client takes the CPU from the ones whose tick has completed (P = 40 at n_max = 180: 6.0e5 with
+     * no poll, 5.5e5 with 20 us, 4.2e5 with 50 us; round 5: 150 us 3.2e5) */
     double spin = c->spin_s;
-    if (spin < 0) spin = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) <= c->cpus ? 150e-6 : 20e-6;
+    if (spin < 0) spin = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) <= c->cpus ? 150e-6 : 0.0;
     const double t0 = now_s();
     for (int i = 0;; ++i) {
         if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == r) {

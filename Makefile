@@ -9,14 +9,14 @@ LIB := $(PKG)/libqcart.so
 # contraction fused differently per instantiation)
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -ffp-contract=on
 OBJS := $(addprefix $(CSRC)/build/,qcart_k_ho.o qcart_k_iho.o qcart_k_grid.o qcart_k_f32.o qcart_k_group.o qcart_record.o qcart_noise.o qcart_replay.o qcart_actor.o qcart_dispatch.o qcart_api.o qcart_tables.o qcart_server.o qcart_env.o)
-HDRS := include/qcart.h $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp $(CSRC)/qcart_shm.h
+HDRS := include/qcart.h $(CSRC)/qcart_mt.hpp $(CSRC)/qcart_expt.hpp $(CSRC)/qcart_kargs.hpp $(CSRC)/qcart_tables.hpp $(CSRC)/qcart_kernels.hpp $(CSRC)/qcart_shm.h
 # the step server's client side: plain C (POSIX shared memory + futexes), no HIP
 CLIENT := $(PKG)/libqcart_client.so
 
 all: $(LIB) $(CLIENT) oracle
 
 $(CLIENT): $(CSRC)/qcart_client.c $(CSRC)/qcart_shm.h include/qcart_client.h Makefile
-	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lrt
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lrt -lm
 
 # kernel TUs: MachineLICM off — it hoists loop-invariant FP64 constants of the step loop's rare
 # noise refill into registers that then spill (same speed, ~0.9 GB less scratch traffic per launch)

@@ -39,7 +39,8 @@ EXPORTS = (
     "qc_replay_create", "qc_replay_destroy", "qc_replay_last_error", "qc_replay_set_stream", "qc_replay_store",
     "qc_replay_store_xp", "qc_replay_sample", "qc_replay_update", "qc_replay_rebuild", "qc_replay_stats",
     "qc_replay_buffers", "qc_set_seed_mt19937_envs", "qc_mt19937_normals",
-    "qc_server_create", "qc_server_run", "qc_server_stop", "qc_server_stats", "qc_server_timing", "qc_server_last_error",
+    "qc_server_create", "qc_server_run", "qc_server_stop", "qc_server_stats", "qc_server_timing", "qc_server_resident",
+    "qc_server_last_error",
     "qc_server_destroy", "qc_env_tail",
 )
 
@@ -207,6 +208,7 @@ def lib() -> ctypes.CDLL:
     L.qc_server_stop.argtypes = [vp]
     L.qc_server_stats.argtypes = [vp, P(i64), P(i64)]
     L.qc_server_timing.argtypes = [vp, vp]
+    L.qc_server_resident.argtypes = [vp, P(i64)]
     L.qc_server_last_error.argtypes = [vp]
     L.qc_server_last_error.restype = ctypes.c_char_p
     L.qc_server_destroy.argtypes = [vp]

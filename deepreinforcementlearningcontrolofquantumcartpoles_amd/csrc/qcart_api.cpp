@@ -36,6 +36,9 @@ void set_create_err(const std::string& s) {
 
 namespace qcart {
 void set_global_error(const std::string& m) { set_create_err(m); }
+// the step server's resident kernel (qcart_server.cpp): declared here, defined after qc_handle
+bool resident_available(const qc_handle* h);
+int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, void* stream);
 }  // namespace qcart
 
 struct qc_handle {
@@ -347,6 +350,37 @@ int validate_params(const qc_params* p, std::string& err) {
 }
 
 }  // namespace
+
+namespace qcart {
+// fp64 Fock modules with a resident kernel instantiated for their rows per lane, in MT19937 mode
+bool resident_available(const qc_handle* h) {
+    return h && h->p.precision == QC_FP64 && h->noise_mode == QC_NOISE_MT19937 && h->d_mt && h->p.batch > 0 &&
+           h->p.batch <= kSpreadBatch && have_resident(h->p.family, h->op.Rs);
+}
+// k_resident over the handle's B envs (env e = slot e): the KArgs of qc_step's short one-step call (MODE 0, one env
+// per block, no grouping) — the same step body and constants, so both paths step an env bitwise alike
+int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, void* stream) {
+    if (!resident_available(h)) return fail(h, QC_EINVAL, "no resident kernel for this module");
+    KArgs a = base_args(h);
+    a.psi = psi;
+    a.n_steps = 1;
+    a.tab_mode = 0;
+    a.lds_bytes = 0;
+    a.lds_img = 0;
+    a.lds_nz = 0;
+    a.spread = 1;
+    a.n_blocks = (uint32_t)h->p.batch;
+    a.bad = nullptr;   // the client sends only actions of the grid (anything else bounces to the tick path)
+    ResArgs r{};
+    r.slots = slots;
+    r.ctl = ctl;
+    r.mt = h->d_mt;
+    r.beat_ticks = (uint64_t)(beat_s * 1e8);   // s_memrealtime: 100 MHz
+    DeviceGuard g(h->device);
+    const int rc = launch_resident(h->p.family, h->op.Rs, a, r, stream);
+    return rc ? fail(h, QC_EHIP, "resident kernel launch failed") : QC_OK;
+}
+}  // namespace qcart
 
 extern "C" {
 

@@ -4,9 +4,13 @@
  * actors each own a CPU-only `simulation` module; here they own one slot of the server's batch).
  * Protocol and layout: qcart_shm.h. A call copies the state into the slot's row, publishes req + 1, and waits
  * (a short spin, then a futex on the header's tick word) until the server has published done = req.
+ * step(state, dt, force, gamma) on the action grid goes to the server's resident kernel when it has one (r_on): the
+ * same row, rreq + 1, and a poll of rdone that the GPU writes (no futex: the GPU cannot wake one; past the usable
+ * CPUs the poll yields its CPU). A request the kernel does not take (QCS_EBOUNCE) is sent through the ticks.
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <math.h>
 #include <fcntl.h>
 #include <linux/futex.h>
 #include <sched.h>
@@ -156,7 +160,8 @@ void qcc_close(qcc* c) {
     /* a request still pending is completed first (its slot must not be re-claimed mid-tick), unless the server is
      * gone; bounded, so a close (also from a destructor) never hangs on a server that stopped answering */
     const double t0 = now_s();
-    while (__atomic_load_n(&c->slot->done, __ATOMIC_ACQUIRE) != __atomic_load_n(&c->slot->req, __ATOMIC_RELAXED) &&
+    while ((__atomic_load_n(&c->slot->done, __ATOMIC_ACQUIRE) != __atomic_load_n(&c->slot->req, __ATOMIC_RELAXED) ||
+            __atomic_load_n(&c->slot->rdone, __ATOMIC_ACQUIRE) != __atomic_load_n(&c->slot->rreq, __ATOMIC_RELAXED)) &&
            !server_gone(c->hdr) && now_s() - t0 < 60.0)
         usleep(100);
     c->slot->pid = 0;
@@ -186,6 +191,52 @@ int qcc_settings(const qcc* c, double* out) {
     out[7] = h->f_max;
     out[8] = h->n_actions;
     return QCC_OK;
+}
+
+/* the force's index on the server's action grid (its slot_of), or -1: off the grid (a custom slot, the ticks) */
+static int grid_action(const qcs_header* h, double force) {
+    const int half = h->n_actions / 2;
+    if (half <= 0) return -1;
+    const double spacing = h->f_max / half;
+    const double a = nearbyint(force / spacing);
+    if (a >= -half && a <= half && a * spacing == force) return (int)a + half;
+    return -1;
+}
+
+/* post the slot's filled request to the resident kernel and poll for its results */
+static int rcall(qcc* c) {
+    qcs_slot* s = c->slot;
+    qcs_header* h = c->hdr;
+    const uint32_t r = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED) + 1u;
+    __atomic_store_n(&s->rreq, r, __ATOMIC_SEQ_CST);
+    /* more clients than usable CPUs: a polling client gives its CPU to the others (sched_yield) */
+    const int yield = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) > c->cpus;
+    double t0 = 0.0, tl = 0.0;
+    for (uint32_t i = 0;; ++i) {
+        if (__atomic_load_n(&s->rdone, __ATOMIC_ACQUIRE) == r) {
+            const int st = s->rstatus;
+            if (st == QCS_EDROPPED) set_err(c, "request dropped by the step server");
+            return st;
+        }
+        if (yield) sched_yield();
+        else __builtin_ia32_pause();
+        if ((i & 255u) == 255u) {
+            const double t = now_s();
+            if (t0 == 0.0) t0 = tl = t;
+            if (t - tl > 0.02) {   /* the server's liveness, as in call() */
+                tl = t;
+                if (server_gone(h)) {
+                    set_err(c, __atomic_load_n(&h->alive, __ATOMIC_ACQUIRE) ? "the step server's process exited"
+                                                                            : "the step server stopped");
+                    return QCC_ENOSERVER;
+                }
+            }
+            if (t - t0 > 600.0) {
+                set_err(c, "no answer from the step server's resident kernel in 600 s");
+                return QCC_ENOSERVER;
+            }
+        }
+    }
 }
 
 /* post the slot's filled request and wait for its results */
@@ -249,7 +300,16 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
     s->dt = dt;
     s->force = force;
     s->gamma = gamma;
-    const int rc = call(c);
+    int rc = QCS_EBOUNCE;
+    const qcs_header* h = c->hdr;
+    if (n == 1 && __atomic_load_n(&h->r_on, __ATOMIC_ACQUIRE) && dt == h->r_dt && gamma == h->r_gamma) {
+        const int act = grid_action(h, force);
+        if (act >= 0) {
+            s->ract = act;
+            rc = rcall(c);
+        }
+    }
+    if (rc == QCS_EBOUNCE) rc = call(c);   /* (a bounced request left the row untouched) */
     if (rc) return rc;
     memcpy(psi, c->psi, bytes);
     if (q) *q = s->q;

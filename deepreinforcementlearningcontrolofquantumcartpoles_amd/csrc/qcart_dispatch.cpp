@@ -59,6 +59,16 @@ int step_dual_img(int family, int R, int precision) {
     return route(family, R, 6, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr);
 }
 
+int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream) {
+    return route(family, R, 7, a, 0, 0.0, (void*)&r, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, stream);
+}
+bool have_resident(int family, int R) {
+    KArgs a{};
+    a.B = 1;
+    return have_kernel(family, R, 0) &&
+           route(family, R, 8, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, nullptr) == 1;
+}
+
 int launch_step(int family, int R, const KArgs& a, void* stream) {
     return route(family, R, 0, a, 0, 0.0, nullptr, 0, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, stream);
 }

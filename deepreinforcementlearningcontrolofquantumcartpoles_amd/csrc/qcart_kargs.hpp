@@ -129,6 +129,24 @@ struct KArgs {
     int32_t spread;            // MODE 0 without order: one env per block (wave 0; the block's other waves idle)
 };
 
+// the step server's resident kernel (k_resident, qcart_server.cpp): the per-request view of ONE step of ONE env that
+// the step body takes in registers (RES) instead of through the KArgs arrays
+struct ResIO {
+    int32_t slot;               // in: the force slot (the request's action)
+    double z0, z1;              // in: the step's two normals (the env's MT19937 stream)
+    double q, xm;               // out: the step's q and x_mean
+    int32_t fail;               // out: Fail (0 / 1)
+};
+// k_resident's second argument (KArgs stays the first: the step loop reads it through the kernarg segment, KAR)
+struct ResArgs {
+    void* slots;                // device address of the shm object's qcs_slot array (qcart_shm.h), slot e = block e
+    const uint32_t* ctl;        // device address of the header's r_quit word; ctl[1] = r_beat
+    uint32_t* mt;               // [B][kMtWords] the handle's MT19937 states (shared with the tick path's kernels)
+    uint64_t beat_ticks;        // s_memrealtime ticks (100 MHz) without a heartbeat change before a wave exits
+};
+int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream);
+bool have_resident(int family, int R);
+
 // measurement-record update (qcart_record.hip, qc_record)
 struct RecArgs {
     const double* q;            // [n_steps][B] step() q outputs of the interval

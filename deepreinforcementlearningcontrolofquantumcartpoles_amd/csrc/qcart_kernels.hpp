@@ -21,6 +21,8 @@
 
 #include "qcart_expt.hpp"
 #include "qcart_kargs.hpp"
+#include "qcart_mt.hpp"
+#include "qcart_shm.h"
 
 namespace qcart {
 
@@ -1239,8 +1241,12 @@ __device__ __forceinline__ decltype(auto) step_kargs(const KArgs& a) {
 // MODE 3: a two-slot block (k_group's remainder workgroups, KArgs::order_mixed): MODE 1 reads (tables in
 // LDS, scan composites from the slot's global block) with both slots' images in LDS, a.lds_img bytes apart;
 // every wave uses its own env's slot and image
-template <int FAM, int R, int MODE, typename RT, bool SKIP>
-__device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, const uint32_t blk) {
+// RES: the step server's resident kernel (k_resident): ONE step of the block's env, its force slot and normals taken
+// from *rio (registers) instead of the KArgs arrays, its q / x_mean / Fail returned in *rio — the arithmetic is the
+// MODE 0 body's, unchanged
+template <int FAM, int R, int MODE, typename RT, bool SKIP, bool RES = false>
+__device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, const uint32_t blk,
+                                          ResIO* rio = nullptr) {
     QC_KSTAMP_ENTRY();
     constexpr int KL = Fam<FAM>::KL;
     constexpr int W = kStepWaves<FAM, R, RT>;   // waves per block
@@ -1291,11 +1297,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
     // a block shares its first env's slot)
     const bool per_wave = MODE == 0 || MODE == 3;
-    int slot = a.actions ? a.actions[(!per_wave || !active) ? e0 : env] : a.default_action;
+    int slot = RES ? rio->slot : (a.actions ? a.actions[(!per_wave || !active) ? e0 : env] : a.default_action);
     slot = __builtin_amdgcn_readfirstlane(slot);
     // ungrouped calls (MODE 0 without k_group, qc_step's short calls): an out-of-range action of an env with a step
     // budget raises the handle's error word here (k_group does it for grouped calls)
-    if (MODE == 0 && a.bad && active && (slot < 0 || slot >= a.n_slots) && lane == 0 &&
+    if (!RES && MODE == 0 && a.bad && active && (slot < 0 || slot >= a.n_slots) && lane == 0 &&
         (!a.env_steps || (a.env_steps[env] > 0 && a.n_steps > 0)))
         a.bad[0] = 1;
     slot = clamp_slot(slot);   // never index out of the tables
@@ -1519,7 +1525,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         QC_STAMP(0);
         if ((k & 63) == 0) {   // lane j: normals of step k + j
             double z0 = 0.0, z1 = 0.0;
-            if (a.noise) {
+            if constexpr (RES) {   // the one step's pair (lane 0: step 0)
+                z0 = lane == 0 ? rio->z0 : 0.0;
+                z1 = lane == 0 ? rio->z1 : 0.0;
+            } else if (a.noise) {
                 const int kk = k + lane;
                 if (kk < n_my) {
                     z0 = a.noise[((size_t)kk * a.B + env) * 2];
@@ -1550,7 +1559,10 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         }
         // go_one_step: IHO/simulation_i.cpp:432-489
         const double dW = r0 * sdt, dZ = (HC ? a.k_dz : sdt * dt * 0.5) * (r0 + r1 * 0.57735026918962576451);   // 1/sqrt(3)
-        if (lane == 0) {
+        if constexpr (RES) {   // (wave-uniform values)
+            rio->q = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
+            rio->xm = (double)xbar;
+        } else if (lane == 0) {
             if (a.q_out) a.q_out[(size_t)k * a.B + env] = (double)xbar + dW * a.inv_sqrt2g * inv_dt;
             if (a.xm_out) a.xm_out[(size_t)k * a.B + env] = (double)xbar;
         }
@@ -2118,7 +2130,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         for (int j = 0; j < R; ++j)
             if (wb + j < N) st_cx<RT>(gpsi + 2 * (wb + j), psi[j]);
     }
-    if (lane == 0) {
+    if constexpr (RES) {
+        rio->fail = fail;
+    } else if (lane == 0) {
         if (a.fail_step) a.fail_step[env] = fail;
         if (a.term_step) a.term_step[env] = term;
         if (!a.noise) a.ctr[env] = ctr0 + (uint64_t)n_my;   // only the in-kernel Philox stream advances
@@ -2160,6 +2174,103 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
         step_body<FAM, R, MODE, RT, false>(a, a.order, blockIdx.x - m);
     } else {
         step_body<FAM, R, MODE, RT, true>(a, a.order, blockIdx.x);
+    }
+}
+
+// ---- the step server's resident kernel ------------------------------------------------------------
+// One 64-lane block per client slot stays on the GPU while the server runs (qcart_server.cpp): the wave polls its
+// slot's rreq word in the device-mapped shared-memory object, and for each request takes the env's next two normals
+// from its MT19937 state (the state the tick path's kernels share), runs ONE step of the MODE 0 body on the slot's
+// row in place and publishes q / x_mean / Fail and rdone = rreq. A call then costs no launch, no submission and no
+// server-thread turn-around (the tick path's 4.2 + ~5 us + completion + 3.1 us publish per tick).
+// Every wave exits on the header's r_quit word or when the server's heartbeat r_beat has not changed for
+// r.beat_ticks (a server thread that stopped without clearing it). Built for the Fock kernels with their rows read
+// at entry (MODE 0 PRE, R <= 8); the grid TU contracts across statements (-ffp-contract=fast), which would round
+// the Box–Muller of qcart_mt.hpp differently from qcart_noise.hip's (the tick path's) — the grid keeps the ticks.
+template <int FAM, int R>
+constexpr bool kResident = FAM <= 1 && R <= 8;
+
+// host-written words: system-scope atomic loads (vector loads that bypass the non-coherent caches: a uniform plain
+// load of the same address would be a scalar load, and the scalar cache is not kept coherent with these writes)
+__device__ __forceinline__ uint32_t ld_sys_u32(const void* p) {
+    return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys_f64(const void* p) {
+    const uint64_t v = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+template <int FAM, int R>
+__global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r) {
+    __shared__ uint32_t mtl[mt::kN];
+    const int e = (int)blockIdx.x, lane = (int)threadIdx.x;
+    qcs_slot* sl = (qcs_slot*)r.slots + e;
+    uint32_t* g = r.mt + (size_t)e * kMtWords;
+    uint32_t served = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rdone));
+    uint32_t beat = __builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl + 1));
+    uint64_t t_beat = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t rq = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rreq));
+        if (rq == served) {
+            if ((it & 7u) == 0u) {
+                if (__builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl))) break;
+                const uint32_t b = __builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl + 1));
+                const uint64_t t = __builtin_amdgcn_s_memrealtime();
+                if (b != beat) {
+                    beat = b;
+                    t_beat = t;
+                } else if (t - t_beat > r.beat_ticks) {
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        // the client's row and request fields (and the tick path's MT19937 writes) are visible from here on
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        ResIO io{};
+        io.slot = (int32_t)__builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->ract));
+        const double dt = ld_sys_f64(&sl->dt), gamma = ld_sys_f64(&sl->gamma);
+        int32_t status = 0;
+        if (!(dt == a.dt && gamma == a.gamma) || io.slot < 0 || io.slot >= a.n_slots) {
+            status = QCS_EBOUNCE;   // not this kernel's dynamics or action grid: the client takes the tick path
+        } else {
+            // the step's pair: words idx .. idx + 3 of the env's stream (normal 2k from words 4k, 4k + 1, normal 2k + 1
+            // from 4k + 2, 4k + 3: k_mt_normals' order), after a twist when the 624 words are used up
+            int idx = (int)__builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(g + mt::kN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            uint32_t w = 0;
+            if (idx >= mt::kN) {
+                for (int i = lane; i < mt::kN; i += 64) mtl[i] = g[i];
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                mt::twist(mtl, lane);
+                for (int i = lane; i < mt::kN; i += 64) g[i] = mtl[i];
+                idx = 0;
+                if (lane < 4) w = mtl[lane];
+            } else if (lane < 4) {
+                w = g[idx + lane];
+            }
+            w = mt::temper(w);
+            const uint32_t w1 = (uint32_t)__shfl((int)w, (2 * lane) & 3), w2 = (uint32_t)__shfl((int)w, (2 * lane + 1) & 3);
+            const double x = mt::boxmuller(w1, w2);
+            io.z0 = readlane_d(x, 0);
+            io.z1 = readlane_d(x, 1);
+            if (lane == 0) g[mt::kN] = (uint32_t)(idx + 4);
+            step_body<FAM, R, 0, double, true, true>(a, nullptr, (uint32_t)e, &io);
+        }
+        if (lane == 0) {
+            sl->q = io.q;
+            sl->xmean = io.xm;
+            sl->fail = io.fail > 0 ? 1 : 0;
+            sl->rstatus = status;
+        }
+        // the row, the results and the stream's state before rdone (every lane's stores: the fence waits on the wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (lane == 0) __hip_atomic_store(&sl->rdone, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        served = rq;
+        t_beat = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -2473,6 +2584,14 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     const dim3 grid(nblocks(a.B)), block(256);
     hipStream_t st = (hipStream_t)stream;
     if (kind == 4) return kStepWaves<FAM, R, RT>;   // query: envs per step workgroup
+    if (kind == 8) return (kResident<FAM, R> && sizeof(RT) == 8) ? 1 : 0;   // query: a resident kernel
+    if (kind == 7) {   // the step server's resident kernel: one 64-lane block per env (slot); `out` is the ResArgs
+        if constexpr (kResident<FAM, R> && sizeof(RT) == 8) {
+            hipLaunchKernelGGL((k_resident<FAM, R>), dim3((unsigned)a.B), dim3(64), 0, st, a, *(const ResArgs*)out);
+            return hipGetLastError() == hipSuccess ? 0 : -3;
+        }
+        return -6;
+    }
     if (kind == 6) return kDual<FAM, R, RT> ? (int)((kDualImg<FAM, R, RT> + 15u) & ~15u) : 0;   // query: MODE 3 image
     if (kind == 0) {
         int rc;

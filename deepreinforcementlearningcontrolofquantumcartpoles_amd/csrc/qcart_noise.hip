@@ -20,25 +20,18 @@
 // words an env actually consumes (2 normals per step it takes), exactly as each reference actor's
 // stream does.
 #include <hip/hip_runtime.h>
-
-constexpr double kMklZeroWordRadius = 3.4244955099270222;   // MKL 2021.4 BOXMULLER at u1 = 0
-
 #include <stdint.h>
 
 #include "qcart_kargs.hpp"
+#include "qcart_mt.hpp"
 
 namespace qcart {
 namespace {
 
-constexpr int kN = 624, kM = 397;
-
-__device__ __forceinline__ uint32_t temper(uint32_t y) {
-    y ^= y >> 11;
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= y >> 18;
-    return y;
-}
+using mt::kM;
+using mt::kN;
+using mt::temper;
+using mt::twist;
 
 // init_by_array({seed}, 1) of mt19937ar.c (the serial part runs on lane 0 over the wave's LDS copy)
 // mask (optional, [B]): only envs with mask[e] != 0 are (re)seeded, the others keep their streams
@@ -69,26 +62,6 @@ __global__ __launch_bounds__(256) void k_mt_seed(const uint32_t* seeds, const ui
     uint32_t* g = st + (size_t)e * kMtWords;
     for (int i = lane; i < kN; i += 64) g[i] = mt[i];
     if (lane == 0) g[kN] = kN;   // read index: the first draw twists
-}
-
-// the generation twist of mt19937ar.c over a wave's LDS state, in 64-lane chunks of increasing k: a
-// chunk reads mt[k], mt[k+1], mt[(k+397) % 624] before any lane of it writes, and everything it reads
-// is exactly what the serial loop would see (old above the chunk, already-new (k+397) % 624 < k)
-__device__ __forceinline__ void twist(uint32_t* mt, int lane) {
-    for (int c = 0; c < kN; c += 64) {
-        const int k = c + lane;
-        uint32_t v = 0;
-        if (k < kN) {
-            const uint32_t y = (mt[k] & 0x80000000u) | (mt[k + 1 == kN ? 0 : k + 1] & 0x7fffffffu);
-            const int m = k + kM < kN ? k + kM : k + kM - kN;
-            v = mt[m] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (k < kN) mt[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
 }
 
 // One wave per env: the env's min(n_steps, env_steps[e]) steps need 4 words each; normals go to
@@ -128,12 +101,7 @@ __global__ __launch_bounds__(256) void k_mt_normals(uint32_t* st, int64_t B, int
         }
         const int avail = (int)((need - done) < (int64_t)(kN - idx) ? (need - done) : (int64_t)(kN - idx));
         for (int p = lane; p < avail / 2; p += 64) {
-            const uint32_t w1 = temper(mt[idx + 2 * p]);
-            const double u1 = (double)w1 * 0x1.0p-32;
-            const double u2 = (double)temper(mt[idx + 2 * p + 1]) * 0x1.0p-32;
-            // a zero first word: MKL returns the finite radius kMklZeroWordRadius, not inf (pinned, below)
-            const double rad = w1 ? sqrt(-2.0 * log(u1)) : kMklZeroWordRadius;
-            const double x = rad * sin(6.283185307179586 * u2);
+            const double x = qcart::mt::boxmuller(temper(mt[idx + 2 * p]), temper(mt[idx + 2 * p + 1]));
             const int64_t n = done / 2 + p + 2 * s0;   // normal index of the env: step n / 2, component n % 2
             noise[((size_t)(n >> 1) * B + e) * 2 + (n & 1)] = x;
         }

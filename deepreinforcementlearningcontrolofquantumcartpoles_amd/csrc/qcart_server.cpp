@@ -5,6 +5,12 @@
 // e): the per-process H2D copy + two launches + D2H copy + sync of the plain drop-in, serialised over P HIP
 // contexts, becomes one set of launches per tick for all of them.
 //
+// The resident path (QCART_SERVER_RESIDENT=0 turns it off): for the Fock modules the server keeps k_resident on the
+// GPU while it runs — one wave per slot polling the slot's rreq word in the device-mapped object — and a client sends
+// its step(state, dt, force, gamma) there directly (on the action grid, at the kernel's dt and gamma): the GPU steps
+// the row in place and publishes rdone; the server thread only keeps the heartbeat and serves everything else by
+// ticks. Table changes (a new dt, an off-grid force slot) stop the kernel first and relaunch it after the tick.
+//
 // A tick: wait until every owned slot has a pending request or batch_wait_us has passed since the first one;
 // copy the pending states into the server's pinned, device-mapped work rows (the kernels read and write them
 // in place: no hipMemcpy); per-env MT19937 reseeds (masked), the step envs grouped by physics-step count and
@@ -23,6 +29,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -34,6 +41,8 @@
 
 namespace qcart {
 void set_global_error(const std::string& m);   // qcart_api.cpp: what qc_last_error(NULL) returns
+bool resident_available(const qc_handle* h);
+int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, void* stream);
 }
 
 namespace {
@@ -100,6 +109,13 @@ struct qc_server {
     // (QCART_SERVER_INPLACE=0, or a failed registration: copies through `psi`)
     double* d_spsi = nullptr;
     bool inplace = false;
+    // the resident path: the whole object registered (d_shm), k_resident on its own stream while run() serves
+    bool resident = false, r_running = false;
+    uint8_t* d_shm = nullptr;
+    hipStream_t rstream = nullptr;
+    hipEvent_t r_exit = nullptr;   // recorded after the resident launch: complete once every wave has exited
+    uint32_t beat = 0;
+    double t_beat = 0;
     // MT19937 prefetch (QCART_SERVER_PREFETCH=0 turns it off): after a tick, every owned env that has no drawn pair
     // draws its next step's pair into d_pre (has_pre = 1) while the clients turn round; a 1-step call then steps on
     // it directly and a 10-step call takes it as its step 0 — the normals kernel leaves the tick's critical path.
@@ -128,6 +144,8 @@ int sfail(qc_server* s, int code, const std::string& msg) {
     return code;
 }
 
+void resident_stop(qc_server* s);
+
 // force -> action slot, as the drop-in (simulation.py _slot): the 21-level grid, else a cached custom slot
 int slot_of(qc_server* s, double force, int& slot) {
     const int half = s->p.n_actions / 2;
@@ -142,6 +160,7 @@ int slot_of(qc_server* s, double force, int& slot) {
         slot = it->second;
         return QC_OK;
     }
+    resident_stop(s);   // the slot tables are rebuilt
     const int rc = qc_add_force(s->h, force);
     if (rc < 0) return rc;
     s->custom[force] = rc;
@@ -149,7 +168,47 @@ int slot_of(qc_server* s, double force, int& slot) {
     return QC_OK;
 }
 
+// the resident kernel (no-ops without the resident path): stopped before anything changes the slot tables or the
+// handle's dynamics, and when run() returns; (re)launched by the serving loop
+void resident_stop(qc_server* s) {
+    if (!s->r_running) return;
+    __atomic_store_n(&s->hdr->r_quit, 1u, __ATOMIC_SEQ_CST);
+    (void)hipStreamSynchronize(s->rstream);   // every wave reaches the quit word within a poll
+    __atomic_store_n(&s->hdr->r_quit, 0u, __ATOMIC_SEQ_CST);
+    s->r_running = false;
+}
+void resident_start(qc_server* s) {
+    if (!s->resident || s->r_running) return;
+    if (s->r_exit && hipEventQuery(s->r_exit) == hipErrorNotReady) return;   // (a previous launch still draining)
+    qcs_header* H = s->hdr;
+    H->r_dt = s->cur_dt;
+    H->r_gamma = s->cur_gamma;
+    __atomic_store_n(&H->r_quit, 0u, __ATOMIC_SEQ_CST);
+    const size_t ctl = offsetof(qcs_header, r_quit);
+    const int rc = qcart::resident_launch(s->h, s->d_spsi, s->d_shm + H->slot_off, (const uint32_t*)(s->d_shm + ctl),
+                                          1.0, s->rstream);
+    if (rc != QC_OK || hipEventRecord(s->r_exit, s->rstream) != hipSuccess) {
+        // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0)
+        __atomic_store_n(&H->r_on, 0u, __ATOMIC_SEQ_CST);
+        s->resident = false;
+        return;
+    }
+    s->r_running = true;
+}
+// the server loop's heartbeat (every 100 us at most) and the kernel's state: exited on its own (a heartbeat gap
+// longer than its limit) -> relaunched
+void resident_tend(qc_server* s, double now) {
+    if (!s->resident) return;
+    if (now - s->t_beat > 100.0) {
+        __atomic_store_n(&s->hdr->r_beat, ++s->beat, __ATOMIC_RELAXED);
+        s->t_beat = now;
+    }
+    if (s->r_running && hipEventQuery(s->r_exit) == hipSuccess) s->r_running = false;
+    if (!s->r_running) resident_start(s);
+}
+
 void free_server(qc_server* s) {
+    resident_stop(s);
     if (s->h) qc_destroy(s->h);
     void* hb[] = {s->psi, s->act, s->st1, s->st10, s->seeds, s->mask, s->q1, s->xm1, s->q10, s->xm10, s->fs1, s->fb10,
                   s->xe, s->obs, s->has_pre, s->gen, s->pf, s->hp};
@@ -157,7 +216,9 @@ void free_server(qc_server* s) {
         if (b) (void)hipHostFree(b);
     if (s->d_pre) (void)hipFree(s->d_pre);
     if (s->d_n10) (void)hipFree(s->d_n10);
-    if (s->inplace && s->shm) (void)hipHostUnregister(s->shm + s->hdr->psi_off);
+    if (s->inplace && s->shm) (void)hipHostUnregister(s->d_shm ? s->shm : s->shm + s->hdr->psi_off);
+    if (s->r_exit) (void)hipEventDestroy(s->r_exit);
+    if (s->rstream) (void)hipStreamDestroy(s->rstream);
     if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->shm) {
@@ -229,6 +290,7 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
             rest = later;
             int rc = QC_OK;
             if (dt != s->cur_dt || gamma != s->cur_gamma) {
+                resident_stop(s);
                 (void)hipStreamSynchronize(s->stream);
                 rc = qc_set_dynamics(s->h, dt, gamma);
                 if (rc == QC_OK) { s->cur_dt = dt; s->cur_gamma = gamma; }
@@ -361,6 +423,12 @@ void reap_dead_clients(qc_server* s) {
         const int32_t pid = __atomic_load_n(&sl.pid, __ATOMIC_ACQUIRE);
         if (!ld_acq(&sl.owner) || pid <= 0) continue;
         if (kill(pid, 0) == 0 || errno != ESRCH) continue;
+        const uint32_t rr = __atomic_load_n(&sl.rreq, __ATOMIC_ACQUIRE);
+        if (rr != __atomic_load_n(&sl.rdone, __ATOMIC_ACQUIRE)) {
+            if (s->r_running) continue;   // the resident wave serves it first (the slot is released afterwards)
+            sl.rstatus = QCS_EDROPPED;
+            __atomic_store_n(&sl.rdone, rr, __ATOMIC_RELEASE);
+        }
         // a pending request is published as dropped, never as served (its state row and results were not written)
         sl.status = QCS_EDROPPED;
         std::snprintf(sl.err, sizeof(sl.err), "request dropped: client process %d exited", (int)pid);
@@ -484,7 +552,24 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
         // frozen env's row unread and unwritten: the rows of clients not in the tick are theirs to write meanwhile
         const char* m = std::getenv("QCART_SERVER_INPLACE");
         const char* m0 = std::getenv("QCART_SHORT_MODE0");
-        if (!(m && std::atoi(m) == 0) && !(m0 && std::atoi(m0) == 0) && P <= 4096 &&
+        const char* mr = std::getenv("QCART_SERVER_RESIDENT");
+        const bool inpl = !(m && std::atoi(m) == 0) && !(m0 && std::atoi(m0) == 0) && P <= 4096;
+        // the resident path: the whole object (header, slots, rows) registered, the kernel's stream and exit event
+        if (inpl && !(mr && std::atoi(mr) == 0) && qcart::resident_available(s->h) &&
+            hipStreamCreateWithFlags(&s->rstream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&s->r_exit, hipEventDisableTiming) == hipSuccess &&
+            hipHostRegister(s->shm, total, hipHostRegisterMapped) == hipSuccess) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, s->shm, 0) == hipSuccess) {
+                s->d_shm = (uint8_t*)d;
+                s->d_spsi = (double*)(s->d_shm + psi_off);
+                s->inplace = true;
+                s->resident = true;
+                s->prefetch = false;   // the resident wave draws each step's pair itself: no pair drawn ahead
+            } else {
+                (void)hipHostUnregister(s->shm);
+            }
+        } else if (inpl &&
             hipHostRegister(s->shm + psi_off, obs_off - psi_off, hipHostRegisterMapped) == hipSuccess) {
             void* d = nullptr;
             if (hipHostGetDevicePointer(&d, s->shm + psi_off, 0) == hipSuccess) {
@@ -518,6 +603,9 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
     H->n_actions = p->n_actions;
     H->server_pid = (int32_t)getpid();
     H->pid_ns = qcs_pid_ns();
+    H->r_on = s->resident ? 1u : 0u;
+    H->r_dt = s->cur_dt;
+    H->r_gamma = s->cur_gamma;
     s->served.assign(P, 0u);
     s->pre_ok.assign(P, 0);
     __atomic_store_n(&H->alive, 1u, __ATOMIC_SEQ_CST);
@@ -532,7 +620,9 @@ int qc_server_run(qc_server* s, double seconds) {
     std::vector<int> pend;
     int owned = 0;
     double idle_since = now_us(), last_reap = now_us();
+    resident_tend(s, now_us());
     while (!s->stop.load(std::memory_order_relaxed) && now_us() < t_end) {
+        resident_tend(s, now_us());
         if (now_us() - last_reap > 100000.0) {   // every 0.1 s
             reap_dead_clients(s);
             last_reap = now_us();
@@ -551,9 +641,10 @@ int qc_server_run(qc_server* s, double seconds) {
             __atomic_store_n(&s->hdr->server_sleeping, 0u, __ATOMIC_SEQ_CST);
             continue;
         }
-        // batch: wait (briefly) for the other owned slots' requests of this tick
+        // batch: wait (briefly) for the other owned slots' requests of this tick (with the resident path the ticks
+        // carry only the rare calls — set_seed, x_expectation, ... — which do not come together: no wait)
         const double t0 = now_us();
-        while ((int)pend.size() < owned && now_us() - t0 < s->wait_us) {
+        while (!s->resident && (int)pend.size() < owned && now_us() - t0 < s->wait_us) {
             for (int i = 0; i < 32; ++i) cpu_relax();
             scan(s, pend, owned);
         }
@@ -561,6 +652,7 @@ int qc_server_run(qc_server* s, double seconds) {
         serve_tick(s, pend);
         idle_since = now_us();
     }
+    resident_stop(s);
     return QC_OK;
 }
 
@@ -585,6 +677,14 @@ int qc_server_timing(const qc_server* s, double* out) {
     out[2] = s->t_gpu;
     out[3] = s->t_publish;
     return QC_OK;
+}
+
+int qc_server_resident(const qc_server* s, int64_t* calls) {
+    if (!s) return QC_EINVAL;
+    int64_t n = 0;
+    for (int e = 0; e < s->P; ++e) n += __atomic_load_n(&s->slots[e].rdone, __ATOMIC_ACQUIRE);
+    if (calls) *calls = n;
+    return s->resident ? 1 : 0;
 }
 
 const char* qc_server_last_error(const qc_server* s) { return s ? s->err.c_str() : ""; }

@@ -19,7 +19,7 @@
 #include <sys/stat.h>
 
 #define QCS_MAGIC 0x56534351u /* "QCSV" */
-#define QCS_VERSION 2u
+#define QCS_VERSION 3u
 #define QCS_MAX_OBS 64        /* >= the largest n_obs ((2+9+1)*9/2 = 54 grid moments) */
 
 /* request operations (the reference module's functions, IHO/simulation_i.cpp:618-631, QO/simulation_quart.cpp:656-668) */
@@ -33,6 +33,8 @@ enum qcs_op {
 };
 
 #define QCS_EDROPPED (-100)   /* a slot status: the server released the slot without serving the request */
+#define QCS_EBOUNCE (-101)    /* a resident-path status: not served there (dt / gamma / action not the resident
+                                 kernel's); the client sends the request through the tick path instead */
 
 typedef struct qcs_header {
     uint32_t magic, version;
@@ -52,6 +54,16 @@ typedef struct qcs_header {
     uint64_t ticks, calls;   /* served ticks / requests (statistics, server-written) */
     uint64_t pid_ns;         /* inode of the server's PID namespace (/proc/self/ns/pid): pids are compared only
                                 inside one namespace, so clients from another are refused */
+    /* the resident path (qcart_server.cpp, k_resident): one wave per slot polls the slot's rreq word in this
+     * device-mapped object and steps the env in place — no launch, no server thread in the call. r_on: the server
+     * has a resident kernel for its module; a client sends step(state, dt, force, gamma) there when dt and gamma
+     * are r_dt / r_gamma and the force is on the action grid (anything else: the tick path) */
+    uint32_t r_on, r_pad0;
+    double r_dt, r_gamma;
+    uint64_t r_pad1[8];      /* r_quit / r_beat on a line of their own: the GPU polls it, the clients never read it */
+    uint32_t r_quit;         /* set by the server: every resident wave exits */
+    uint32_t r_beat;         /* the server loop's heartbeat: the waves exit after ~1 s without a change */
+    uint64_t r_pad2[7];
 } qcs_header;
 
 typedef struct qcs_slot {
@@ -68,7 +80,11 @@ typedef struct qcs_slot {
     double q, xmean;         /* step: the last step's q and x_mean */
     double value;            /* x_expectation */
     char err[96];
-    uint8_t pad[32];
+    uint32_t rreq;           /* the resident path's request sequence number (client) */
+    uint32_t rdone;          /* = rreq once the resident wave has written the results (device) */
+    int32_t ract;            /* the request's action slot (the force's index on the action grid) */
+    int32_t rstatus;         /* 0, or QCS_EBOUNCE / QCS_EDROPPED */
+    uint8_t pad[16];
 } qcs_slot;
 
 /* inode of this process's PID namespace (0 if /proc is unavailable) */

@@ -470,7 +470,9 @@ int qc_env_tail(qc_handle* h, const qc_env_tail_args* a);
  * x_expectation / get_moments requests. Each tick steps every pending env in one batched launch (per-env step
  * budgets keep the others frozen); the tick waits up to batch_wait_us (<= 0: 40 us) after its first request for
  * the other owned slots' requests. Results equal the plain drop-in's (the same kernels, the same per-env
- * MT19937 stream). */
+ * MT19937 stream). Fock modules: while qc_server_run serves, a resident kernel (one wave per slot) answers the
+ * clients' step(state, dt, force, gamma) calls on the action grid directly from the shared object, without a
+ * launch or a tick (qcart_shm.h); the ticks carry the other calls. */
 typedef struct qc_server qc_server;
 int qc_server_create(const qc_params* p, int device, int32_t max_clients, const char* name, double batch_wait_us,
                      qc_server** out);
@@ -481,6 +483,9 @@ int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls);
 /* out[4]: microseconds summed over the ticks — batching wait, host launches, GPU (until the stream sync
  * returned), publishing the results */
 int qc_server_timing(const qc_server* s, double* out);
+/* 1 when the server serves one-step calls on its resident kernel (Fock modules; QCART_SERVER_RESIDENT=0 turns it
+ * off), else 0; *calls: the requests the resident path has answered since the object was created */
+int qc_server_resident(const qc_server* s, int64_t* calls);
 const char* qc_server_last_error(const qc_server* s);
 /* marks the object dead (waiting clients fail with QCC_ENOSERVER) and unlinks it */
 void qc_server_destroy(qc_server* s);

@@ -87,10 +87,14 @@ def test_served_simulate_10_steps_matches_oracle(served, oracle_mod):
     TN.test_dropin_simulate_10_steps_matches_oracle(oracle_mod)
 
 
-def test_concurrent_clients_equal_the_plain_dropin():
-    """Four clients on one server, each in its own thread (the ctypes calls release the GIL, so the ticks batch
-    several envs), each its own seed and forces: every state bitwise equal to the plain drop-in's run of the same
-    sequence, and the x_expectation served in the same ticks."""
+@pytest.mark.parametrize("resident", [True, False])
+def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, resident):
+    """Four clients on one server, each in its own thread (the ctypes calls release the GIL), each its own seed and
+    forces: every state bitwise equal to the plain drop-in's run of the same sequence, and the x_expectation served
+    in the same ticks. resident: the step calls go to the resident kernel (one wave per slot polling the shared
+    object); else (QCART_SERVER_RESIDENT=0) every call is batched into the ticks."""
+    if not resident:
+        monkeypatch.setenv("QCART_SERVER_RESIDENT", "0")
     n_max, P, steps = 180, 4, 240
     dt, gamma = 1 / 1440, 2 * pi
     plain = S.load(cfg.IHO, n_max=n_max)
@@ -131,8 +135,12 @@ def test_concurrent_clients_equal_the_plain_dropin():
         assert np.array_equal(got[c][0], want[c][0]), c
         assert got[c][1] == want[c][1], c
         assert got[c][2] == want[c][2], c
-    assert stats["calls"] == P * (steps + 3)          # set_seed(0) at open, set_seed, steps, x_expectation
-    assert stats["ticks"] < stats["calls"]            # ticks served several envs at once
+    assert stats["resident"] == resident
+    if resident:                                      # the steps on the resident kernel, the rest in ticks
+        assert stats["resident_calls"] == P * steps and stats["calls"] == P * 3
+    else:
+        assert stats["calls"] == P * (steps + 3)      # set_seed(0) at open, set_seed, steps, x_expectation
+        assert stats["ticks"] < stats["calls"]        # ticks served several envs at once
 
 
 def _mixed_calls(m, c, n_max, dt, gamma):
@@ -181,6 +189,55 @@ def test_served_mixed_calls_keep_the_streams_of_the_plain_dropin():
     for c in range(P):
         assert np.array_equal(got[c][0], want[c][0]), c
         assert got[c][1] == want[c][1], c
+
+
+def _table_change_calls(m, c, n_max, dt, gamma):
+    """Steps on the action grid (the resident kernel) with an off-grid force every 25th call (a new custom slot: the
+    server stops the resident kernel, rebuilds the slot tables, serves the call in a tick and relaunches) and a gamma
+    change half way (the kernel's dynamics: stopped, relaunched with the new gamma)."""
+    m.set_seed(500 + c)
+    st = np.zeros(n_max + 1, np.complex128)
+    st[0] = 1.0
+    out = []
+    for k in range(100):
+        F = 0.8 * ((k // 30 + c) % 3 - 1)
+        if k % 25 == 7:
+            F = 0.37 + 0.11 * c + 0.01 * k
+        g = gamma if k < 50 else gamma / 2
+        out.append(tuple(m.step(st, dt, F, g)))
+    out.append(m.x_expectation(st))
+    return st.copy(), out
+
+
+def test_resident_kernel_survives_table_changes_bitwise():
+    """Two clients stepping concurrently while the other one's off-grid forces and gamma change stop and relaunch the
+    resident kernel: every state and return bitwise the plain drop-in's, and most steps on the resident path."""
+    n_max, P = 180, 2
+    dt, gamma = 1 / 1440, 2 * pi
+    plain = S.load(cfg.IHO, n_max=n_max)
+    want = [_table_change_calls(plain, c, n_max, dt, gamma) for c in range(P)]
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=P, name=name, n_max=n_max).start()
+    got = [None] * P
+    errs = []
+
+    def run(c):
+        try:
+            m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max), name)
+            got[c] = _table_change_calls(m, c, n_max, dt, gamma)
+            m.close()
+        except Exception as e:   # reported below
+            errs.append(repr(e))
+    ts = [threading.Thread(target=run, args=(c,)) for c in range(P)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    stats = srv.stats()
+    srv.close()
+    assert not errs, errs
+    for c in range(P):
+        assert np.array_equal(got[c][0], want[c][0]), c
+        assert got[c][1] == want[c][1], c
+    assert stats["resident"] and stats["resident_calls"] >= P * 80, stats
 
 
 def test_served_errors():
@@ -313,7 +370,7 @@ def test_server_name_collision_and_stale_objects():
     name2 = _name()
     with open("/dev/shm" + name2, "wb") as f:
         h = Header()
-        h.magic, h.version, h.alive, h.server_pid = 0x56534351, 2, 1, dead.pid
+        h.magic, h.version, h.alive, h.server_pid = 0x56534351, 3, 1, dead.pid
         h.pid_ns = os.stat("/proc/self/ns/pid").st_ino
         f.write(bytes(h))
         f.truncate(8192)

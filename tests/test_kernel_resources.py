@@ -146,3 +146,25 @@ def test_metric_kernel_budget(step_kernels):
     """The metric kernel (IHO N = 512, two waves per SIMD): <= 256 VGPRs, <= 12 B of scratch."""
     v, s, scr, sp, ssp = step_kernels[(1, 8, 2, "d", 1)]
     assert v <= 256 and scr <= 12 and sp <= 2 and ssp <= 7
+
+
+# the step server's resident kernels (k_resident<family, R>: the MODE 0 step body inside a polling loop, one wave per
+# slot, fp64 Fock families with R <= 8): no VGPR spills, and SGPR spills at most these ceilings (the loop's own state
+# and the request fields sit beside the step's constants)
+RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)EE")
+RESIDENT_SGPR_SPILLS = {(0, 1): 46, (0, 2): 40, (0, 4): 54, (0, 8): 64,
+                        (1, 1): 56, (1, 2): 48, (1, 3): 52, (1, 4): 57, (1, 8): 72}
+
+
+def test_resident_kernels_budget():
+    if not os.path.exists(LIB):
+        pytest.skip("libqcart.so not built")
+    import kernel_resources as K
+    got = {}
+    for name, v, s, scr, sp, ssp in K.kernels(LIB):
+        m = RESIDENT.search(name)
+        if m:
+            got[(int(m.group(1)), int(m.group(2)))] = (int(v), int(sp), int(ssp))
+    assert set(got) == set(RESIDENT_SGPR_SPILLS)
+    for k, (v, sp, ssp) in got.items():
+        assert v <= 512 and sp == 0 and ssp <= RESIDENT_SGPR_SPILLS[k], (k, v, sp, ssp)

@@ -2184,11 +2184,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
 // row in place and publishes q / x_mean / Fail and rdone = rreq. A call then costs no launch, no submission and no
 // server-thread turn-around (the tick path's 4.2 + ~5 us + completion + 3.1 us publish per tick).
 // Every wave exits on the header's r_quit word or when the server's heartbeat r_beat has not changed for
-// r.beat_ticks (a server thread that stopped without clearing it). Built for the Fock kernels with their rows read
-// at entry (MODE 0 PRE, R <= 8); the grid TU contracts across statements (-ffp-contract=fast), which would round
-// the Box–Muller of qcart_mt.hpp differently from qcart_noise.hip's (the tick path's) — the grid keeps the ticks.
+// r.beat_ticks (a server thread that stopped without clearing it). Built for the fp64 kernels of the drivers' sizes
+// (Fock R <= 8, grid R <= 9). The grid TU contracts across statements (-ffp-contract=fast-honor-pragmas): the
+// Box–Muller of qcart_mt.hpp carries `fp contract(on)`, and the backend fuses only what the front end marked, so the
+// normals round as in qcart_noise.hip (the tick path's) in every TU.
 template <int FAM, int R>
-constexpr bool kResident = FAM <= 1 && R <= 8;
+constexpr bool kResident = (FAM <= 1 && R <= 8) || (FAM == 2 && R <= 9);
 
 // host-written words: system-scope atomic loads (vector loads that bypass the non-coherent caches: a uniform plain
 // load of the same address would be a scalar load, and the scalar cache is not kept coherent with these writes)

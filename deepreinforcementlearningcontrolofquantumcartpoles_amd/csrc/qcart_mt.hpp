@@ -43,6 +43,8 @@ __device__ __forceinline__ void twist(uint32_t* mt, int lane) {
 // one N(0, 1) from two consecutive tempered words, u = bits * 2^-32: sqrt(-2 ln u1) sin(2 pi u2); a zero first word
 // gives MKL's finite radius, not inf (tests/golden/mkl_v2.npz "zero/*")
 __device__ __forceinline__ double boxmuller(uint32_t w1, uint32_t w2) {
+    // contraction as in qcart_noise.hip whatever the including TU's mode (the grid TU's fast-honor-pragmas)
+#pragma clang fp contract(on)
     const double u1 = (double)w1 * 0x1.0p-32;
     const double u2 = (double)w2 * 0x1.0p-32;
     const double rad = w1 ? sqrt(-2.0 * log(u1)) : kMklZeroWordRadius;

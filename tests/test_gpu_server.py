@@ -240,6 +240,55 @@ def test_resident_kernel_survives_table_changes_bitwise():
     assert stats["resident"] and stats["resident_calls"] >= P * 80, stats
 
 
+def _grid_calls(m, c, ph, gamma):
+    """A grid driver's calls: set_seed, steps at action-grid forces (the resident kernel), get_moments every 20th."""
+    m.set_seed(700 + c)
+    rng = np.random.default_rng(c)
+    x = (np.arange(ph.dim) - ph.dim // 2) * ph.grid_size
+    st = np.exp(-(x - 0.3 * c) ** 2 / 2).astype(np.complex128)
+    st /= np.sqrt((np.abs(st) ** 2).sum() * ph.grid_size)
+    out = []
+    for k in range(120):
+        out.append(tuple(m.step(st, 1 / ph.time_steps, ph.force(int(rng.integers(ph.n_actions))), gamma)))
+        if k % 20 == 19:
+            data = np.zeros(ph.n_obs, np.float64)
+            m.get_moments(st, data)
+            out.append(tuple(data))
+    return st.copy(), out
+
+
+@pytest.mark.parametrize("family", [cfg.QO, cfg.IQO])
+def test_grid_clients_equal_the_plain_dropin(family):
+    """The quartic grid modules at the drivers' sizes (QO x_n = 171, IQO x_n = 521: the R = 3 and R = 9 resident
+    kernels) with three concurrent clients: states, returns and moments bitwise the plain drop-in's."""
+    ph = cfg.DEFAULTS[family]
+    P = 3
+    plain = S.load(family)
+    want = [_grid_calls(plain, c, ph, ph.gamma) for c in range(P)]
+    name = _name()
+    srv = S.StepServer(family, max_clients=P, name=name).start()
+    got = [None] * P
+    errs = []
+
+    def run(c):
+        try:
+            m = S._ServedSimulation(ph, name)
+            got[c] = _grid_calls(m, c, ph, ph.gamma)
+            m.close()
+        except Exception as e:   # reported below
+            errs.append(repr(e))
+    ts = [threading.Thread(target=run, args=(c,)) for c in range(P)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    stats = srv.stats()
+    srv.close()
+    assert not errs, errs
+    for c in range(P):
+        assert np.array_equal(got[c][0], want[c][0]), c
+        assert got[c][1] == want[c][1], c
+    assert stats["resident"] and stats["resident_calls"] == P * 120, stats
+
+
 def test_served_errors():
     """A module whose parameters differ from the server's is refused at load (the drivers' check_settings
     handshake); a full server refuses one more client; a stopped server fails a waiting call."""

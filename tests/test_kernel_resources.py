@@ -149,11 +149,12 @@ def test_metric_kernel_budget(step_kernels):
 
 
 # the step server's resident kernels (k_resident<family, R>: the MODE 0 step body inside a polling loop, one wave per
-# slot, fp64 Fock families with R <= 8): no VGPR spills, and SGPR spills at most these ceilings (the loop's own state
+# slot, fp64: Fock R <= 8, grid R <= 9): no VGPR spills, and SGPR spills at most these ceilings (the loop's own state
 # and the request fields sit beside the step's constants)
 RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)EE")
 RESIDENT_SGPR_SPILLS = {(0, 1): 46, (0, 2): 40, (0, 4): 54, (0, 8): 64,
-                        (1, 1): 56, (1, 2): 48, (1, 3): 52, (1, 4): 57, (1, 8): 72}
+                        (1, 1): 56, (1, 2): 48, (1, 3): 52, (1, 4): 57, (1, 8): 72,
+                        (2, 1): 132, (2, 2): 142, (2, 3): 166, (2, 5): 210, (2, 9): 301}
 
 
 def test_resident_kernels_budget():

@@ -208,7 +208,7 @@ def lib() -> ctypes.CDLL:
     L.qc_server_stop.argtypes = [vp]
     L.qc_server_stats.argtypes = [vp, P(i64), P(i64)]
     L.qc_server_timing.argtypes = [vp, vp]
-    L.qc_server_resident.argtypes = [vp, P(i64)]
+    L.qc_server_resident.argtypes = [vp, P(i64), P(i64)]
     L.qc_server_last_error.argtypes = [vp]
     L.qc_server_last_error.restype = ctypes.c_char_p
     L.qc_server_destroy.argtypes = [vp]

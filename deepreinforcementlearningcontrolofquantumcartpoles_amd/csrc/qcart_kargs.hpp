@@ -143,6 +143,7 @@ struct ResArgs {
     const uint32_t* ctl;        // device address of the header's r_quit word; ctl[1] = r_beat
     uint32_t* mt;               // [B][kMtWords] the handle's MT19937 states (shared with the tick path's kernels)
     uint64_t beat_ticks;        // s_memrealtime ticks (100 MHz) without a heartbeat change before a wave exits
+    uint64_t lease_ticks;       // s_memrealtime ticks after which an idle wave exits (the server relaunches the kernel)
 };
 int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream);
 bool have_resident(int family, int R);

@@ -2183,8 +2183,10 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
 // from its MT19937 state (the state the tick path's kernels share), runs ONE step of the MODE 0 body on the slot's
 // row in place and publishes q / x_mean / Fail and rdone = rreq. A call then costs no launch, no submission and no
 // server-thread turn-around (the tick path's 4.2 + ~5 us + completion + 3.1 us publish per tick).
-// Every wave exits on the header's r_quit word or when the server's heartbeat r_beat has not changed for
-// r.beat_ticks (a server thread that stopped without clearing it). Built for the fp64 kernels of the drivers' sizes
+// Every wave exits on the header's r_quit word, when the server's heartbeat r_beat has not changed for r.beat_ticks
+// (a server thread that stopped without clearing it), or at its first idle poll after r.lease_ticks: a launch lives a
+// bounded time (the server relaunches it at once), so a device-wide synchronisation elsewhere in the server process
+// (hipDeviceSynchronize, a freeing call) waits at most one lease. Built for the fp64 kernels of the drivers' sizes
 // (Fock R <= 8, grid R <= 9). The grid TU contracts across statements (-ffp-contract=fast-honor-pragmas): the
 // Box–Muller of qcart_mt.hpp carries `fp contract(on)`, and the backend fuses only what the front end marked, so the
 // normals round as in qcart_noise.hip (the tick path's) in every TU.
@@ -2211,6 +2213,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
     uint32_t served = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rdone));
     uint32_t beat = __builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl + 1));
     uint64_t t_beat = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t_end = t_beat + r.lease_ticks;
     for (uint32_t it = 0;; ++it) {
         const uint32_t rq = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rreq));
         if (rq == served) {
@@ -2224,6 +2227,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
                 } else if (t - t_beat > r.beat_ticks) {
                     break;
                 }
+                if (t > t_end) break;
             }
             __builtin_amdgcn_s_sleep(2);
             continue;

@@ -26,6 +26,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -42,7 +43,8 @@
 namespace qcart {
 void set_global_error(const std::string& m);   // qcart_api.cpp: what qc_last_error(NULL) returns
 bool resident_available(const qc_handle* h);
-int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, void* stream);
+int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, double lease_s,
+                    void* stream);
 }
 
 namespace {
@@ -116,6 +118,10 @@ struct qc_server {
     hipEvent_t r_exit = nullptr;   // recorded after the resident launch: complete once every wave has exited
     uint32_t beat = 0;
     double t_beat = 0;
+    // a launch's lease (QCART_RESIDENT_LEASE_MS, default 20 ms): its waves exit at their first idle poll after it and
+    // the loop relaunches at once, so a device-wide synchronisation in this process never waits longer
+    double lease_us = 20000.0, t_lease = 0;
+    int64_t launches = 0;
     // MT19937 prefetch (QCART_SERVER_PREFETCH=0 turns it off): after a tick, every owned env that has no drawn pair
     // draws its next step's pair into d_pre (has_pre = 1) while the clients turn round; a 1-step call then steps on
     // it directly and a 10-step call takes it as its step 0 — the normals kernel leaves the tick's critical path.
@@ -186,7 +192,7 @@ void resident_start(qc_server* s) {
     __atomic_store_n(&H->r_quit, 0u, __ATOMIC_SEQ_CST);
     const size_t ctl = offsetof(qcs_header, r_quit);
     const int rc = qcart::resident_launch(s->h, s->d_spsi, s->d_shm + H->slot_off, (const uint32_t*)(s->d_shm + ctl),
-                                          1.0, s->rstream);
+                                          1.0, s->lease_us * 1e-6, s->rstream);
     if (rc != QC_OK || hipEventRecord(s->r_exit, s->rstream) != hipSuccess) {
         // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0)
         __atomic_store_n(&H->r_on, 0u, __ATOMIC_SEQ_CST);
@@ -194,6 +200,8 @@ void resident_start(qc_server* s) {
         return;
     }
     s->r_running = true;
+    s->t_lease = now_us() + s->lease_us;
+    s->launches++;
 }
 // the server loop's heartbeat (every 100 us at most) and the kernel's state: exited on its own (a heartbeat gap
 // longer than its limit) -> relaunched
@@ -553,6 +561,7 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
         const char* m = std::getenv("QCART_SERVER_INPLACE");
         const char* m0 = std::getenv("QCART_SHORT_MODE0");
         const char* mr = std::getenv("QCART_SERVER_RESIDENT");
+        if (const char* ml = std::getenv("QCART_RESIDENT_LEASE_MS")) s->lease_us = std::max(0.05, std::atof(ml)) * 1e3;
         const bool inpl = !(m && std::atoi(m) == 0) && !(m0 && std::atoi(m0) == 0) && P <= 4096;
         // the resident path: the whole object (header, slots, rows) registered, the kernel's stream and exit event
         if (inpl && !(mr && std::atoi(mr) == 0) && qcart::resident_available(s->h) &&
@@ -633,11 +642,14 @@ int qc_server_run(qc_server* s, double seconds) {
                 for (int i = 0; i < 64; ++i) cpu_relax();
                 continue;
             }
-            // asleep until a client kicks (or 2 ms): a client posting while server_sleeping is set wakes us
+            // asleep until a client kicks (or 2 ms; with a resident kernel until its lease is up, then in 20 us steps
+            // until it has drained): a client posting while server_sleeping is set wakes us
             const uint32_t k = __atomic_load_n(&s->hdr->kick, __ATOMIC_SEQ_CST);
             __atomic_store_n(&s->hdr->server_sleeping, 1u, __ATOMIC_SEQ_CST);
             scan(s, pend, owned);
-            if (pend.empty()) futex_wait(&s->hdr->kick, k, 2000000L);
+            long ns = 2000000L;
+            if (s->r_running) ns = std::min(ns, std::max(20000L, (long)((s->t_lease - now_us()) * 1e3)));
+            if (pend.empty()) futex_wait(&s->hdr->kick, k, ns);
             __atomic_store_n(&s->hdr->server_sleeping, 0u, __ATOMIC_SEQ_CST);
             continue;
         }
@@ -679,11 +691,12 @@ int qc_server_timing(const qc_server* s, double* out) {
     return QC_OK;
 }
 
-int qc_server_resident(const qc_server* s, int64_t* calls) {
+int qc_server_resident(const qc_server* s, int64_t* calls, int64_t* launches) {
     if (!s) return QC_EINVAL;
     int64_t n = 0;
     for (int e = 0; e < s->P; ++e) n += __atomic_load_n(&s->slots[e].rdone, __ATOMIC_ACQUIRE);
     if (calls) *calls = n;
+    if (launches) *launches = s->launches;
     return s->resident ? 1 : 0;
 }
 

@@ -366,10 +366,11 @@ class StepServer:
         self._L.qc_server_stats(self._h, ctypes.byref(t), ctypes.byref(c))
         tm = (ctypes.c_double * 4)()
         self._L.qc_server_timing(self._h, tm)
-        rc = ctypes.c_int64()
-        res = self._L.qc_server_resident(self._h, ctypes.byref(rc))
+        rc, rl = ctypes.c_int64(), ctypes.c_int64()
+        res = self._L.qc_server_resident(self._h, ctypes.byref(rc), ctypes.byref(rl))
         n = max(1, t.value)
         return {"ticks": t.value, "calls": c.value, "resident": bool(res == 1), "resident_calls": rc.value,
+                "resident_launches": rl.value,
                 "us_per_tick": {
             "batch_wait": tm[0] / n, "launch": tm[1] / n, "gpu": tm[2] / n, "publish": tm[3] / n}}
 

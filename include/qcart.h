@@ -483,9 +483,10 @@ int qc_server_stats(const qc_server* s, int64_t* ticks, int64_t* calls);
 /* out[4]: microseconds summed over the ticks — batching wait, host launches, GPU (until the stream sync
  * returned), publishing the results */
 int qc_server_timing(const qc_server* s, double* out);
-/* 1 when the server serves one-step calls on its resident kernel (Fock modules; QCART_SERVER_RESIDENT=0 turns it
- * off), else 0; *calls: the requests the resident path has answered since the object was created */
-int qc_server_resident(const qc_server* s, int64_t* calls);
+/* 1 when the server serves one-step calls on its resident kernel (fp64 modules at the drivers' sizes;
+ * QCART_SERVER_RESIDENT=0 turns it off), else 0; *calls: the requests the resident path has answered since the object
+ * was created; *launches: resident kernel launches (each lives one lease, QCART_RESIDENT_LEASE_MS, default 20 ms) */
+int qc_server_resident(const qc_server* s, int64_t* calls, int64_t* launches);
 const char* qc_server_last_error(const qc_server* s);
 /* marks the object dead (waiting clients fail with QCC_ENOSERVER) and unlinks it */
 void qc_server_destroy(qc_server* s);

@@ -87,14 +87,18 @@ def test_served_simulate_10_steps_matches_oracle(served, oracle_mod):
     TN.test_dropin_simulate_10_steps_matches_oracle(oracle_mod)
 
 
-@pytest.mark.parametrize("resident", [True, False])
-def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, resident):
+@pytest.mark.parametrize("mode", ["resident", "short_lease", "ticks"])
+def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
     """Four clients on one server, each in its own thread (the ctypes calls release the GIL), each its own seed and
     forces: every state bitwise equal to the plain drop-in's run of the same sequence, and the x_expectation served
     in the same ticks. resident: the step calls go to the resident kernel (one wave per slot polling the shared
-    object); else (QCART_SERVER_RESIDENT=0) every call is batched into the ticks."""
+    object); short_lease: each launch lives 0.3 ms, so the calls straddle many relaunches; ticks
+    (QCART_SERVER_RESIDENT=0): every call is batched into the ticks."""
+    resident = mode != "ticks"
     if not resident:
         monkeypatch.setenv("QCART_SERVER_RESIDENT", "0")
+    if mode == "short_lease":
+        monkeypatch.setenv("QCART_RESIDENT_LEASE_MS", "0.3")
     n_max, P, steps = 180, 4, 240
     dt, gamma = 1 / 1440, 2 * pi
     plain = S.load(cfg.IHO, n_max=n_max)
@@ -138,6 +142,8 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, resident):
     assert stats["resident"] == resident
     if resident:                                      # the steps on the resident kernel, the rest in ticks
         assert stats["resident_calls"] == P * steps and stats["calls"] == P * 3
+        if mode == "short_lease":
+            assert stats["resident_launches"] >= 10, stats
     else:
         assert stats["calls"] == P * (steps + 3)      # set_seed(0) at open, set_seed, steps, x_expectation
         assert stats["ticks"] < stats["calls"]        # ticks served several envs at once
@@ -287,6 +293,47 @@ def test_grid_clients_equal_the_plain_dropin(family):
         assert np.array_equal(got[c][0], want[c][0]), c
         assert got[c][1] == want[c][1], c
     assert stats["resident"] and stats["resident_calls"] == P * 120, stats
+
+
+def test_device_synchronize_in_the_server_process_returns():
+    """A device-wide synchronisation in the server's own process (torch.cuda.synchronize, i.e. hipDeviceSynchronize,
+    which waits for every stream, the resident kernel's too) while a client steps: it returns within about one lease
+    (20 ms) instead of waiting for a kernel that never ends, and the client's calls go on."""
+    import time
+    n_max = 180
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=1, name=name, n_max=n_max).start()
+    done, errs = [], []
+
+    def run():
+        try:
+            m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max), name)
+            st = np.zeros(n_max + 1, np.complex128)
+            for k in range(3000):
+                if k % 80 == 0:
+                    st[:] = 0
+                    st[0] = 1
+                m.step(st, 1 / 1440, 0.8, 2 * pi)
+            m.close()
+            done.append(True)
+        except Exception as e:   # reported below
+            errs.append(repr(e))
+    t = threading.Thread(target=run)
+    t.start()
+    waits = []
+    try:
+        for _ in range(10):
+            time.sleep(0.005)
+            t0 = time.monotonic()
+            torch.cuda.synchronize()
+            waits.append(time.monotonic() - t0)
+        t.join(timeout=60)
+        stats = srv.stats()
+    finally:
+        srv.close()
+    assert not errs and done, errs
+    assert max(waits) < 0.5, waits
+    assert stats["resident"] and stats["resident_calls"] >= 3000, stats
 
 
 def test_served_errors():

@@ -203,11 +203,12 @@ static int grid_action(const qcs_header* h, double force) {
     return -1;
 }
 
-/* post the slot's filled request to the resident kernel and poll for its results */
-static int rcall(qcc* c) {
+/* post a resident request (the whole request in the rreq word, qcart_shm.h QCS_RQ) and poll for its results */
+static int rcall(qcc* c, int act, uint32_t gen) {
     qcs_slot* s = c->slot;
     qcs_header* h = c->hdr;
-    const uint32_t r = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED) + 1u;
+    const uint32_t prev = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED);
+    const uint32_t r = QCS_RQ((prev & 0xfffu) + 1u, act, gen, s->repoch);
     __atomic_store_n(&s->rreq, r, __ATOMIC_SEQ_CST);
     /* more clients than usable CPUs: a polling client gives its CPU to the others (sched_yield) */
     const int yield = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) > c->cpus;
@@ -302,14 +303,17 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
     s->gamma = gamma;
     int rc = QCS_EBOUNCE;
     const qcs_header* h = c->hdr;
-    if (n == 1 && __atomic_load_n(&h->r_on, __ATOMIC_ACQUIRE) && dt == h->r_dt && gamma == h->r_gamma) {
+    if (n == 1 && __atomic_load_n(&h->r_on, __ATOMIC_ACQUIRE)) {
+        /* dt and gamma as the server's under generation gen: the request carries gen, and a resident kernel of
+         * another generation bounces it */
+        const uint32_t gen = __atomic_load_n(&h->r_gen, __ATOMIC_ACQUIRE);
         const int act = grid_action(h, force);
-        if (act >= 0) {
-            s->ract = act;
-            rc = rcall(c);
-        }
+        if (act >= 0 && dt == h->r_dt && gamma == h->r_gamma) rc = rcall(c, act, gen);
     }
-    if (rc == QCS_EBOUNCE) rc = call(c);   /* (a bounced request left the row untouched) */
+    if (rc == QCS_EBOUNCE) {   /* the ticks (a bounced request left the row untouched); they take stream words */
+        s->repoch++;
+        rc = call(c);
+    }
     if (rc) return rc;
     memcpy(psi, c->psi, bytes);
     if (q) *q = s->q;
@@ -322,6 +326,7 @@ int qcc_set_seed(qcc* c, uint32_t seed) {
     if (!c) return QCC_EINVAL;
     c->slot->op = QCS_OP_SET_SEED;
     c->slot->seed = seed;
+    c->slot->repoch++;   /* a pair the resident wave drew ahead belongs to the old stream */
     return call(c);
 }
 

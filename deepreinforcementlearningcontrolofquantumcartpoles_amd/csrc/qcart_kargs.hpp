@@ -144,6 +144,7 @@ struct ResArgs {
     uint32_t* mt;               // [B][kMtWords] the handle's MT19937 states (shared with the tick path's kernels)
     uint64_t beat_ticks;        // s_memrealtime ticks (100 MHz) without a heartbeat change before a wave exits
     uint64_t lease_ticks;       // s_memrealtime ticks after which an idle wave exits (the server relaunches the kernel)
+    uint32_t gen;               // the server's dynamics generation (6 bits): a request of another one bounces
 };
 int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream);
 bool have_resident(int family, int R);

@@ -2179,10 +2179,12 @@ __attribute__((amdgpu_waves_per_eu((kStepWaves<FAM, R, RT> / 4), (kStepWaves<FAM
 
 // ---- the step server's resident kernel ------------------------------------------------------------
 // One 64-lane block per client slot stays on the GPU while the server runs (qcart_server.cpp): the wave polls its
-// slot's rreq word in the device-mapped shared-memory object, and for each request takes the env's next two normals
-// from its MT19937 state (the state the tick path's kernels share), runs ONE step of the MODE 0 body on the slot's
-// row in place and publishes q / x_mean / Fail and rdone = rreq. A call then costs no launch, no submission and no
-// server-thread turn-around (the tick path's 4.2 + ~5 us + completion + 3.1 us publish per tick).
+// slot's rreq word in the device-mapped shared-memory object — the whole request in that one word (qcart_shm.h
+// QCS_RQ: sequence, action, dynamics generation, stream epoch) — and for each request takes the env's next two
+// normals from its MT19937 state (the state the tick path's kernels share; drawn ahead while the client turns round),
+// runs ONE step of the MODE 0 body on the slot's row in place and publishes q / x_mean / Fail and rdone = rreq. A call
+// then costs no launch, no submission and no server-thread turn-around (the tick path's 4.2 + ~5 us + completion +
+// 3.1 us publish per tick).
 // Every wave exits on the header's r_quit word, when the server's heartbeat r_beat has not changed for r.beat_ticks
 // (a server thread that stopped without clearing it), or at its first idle poll after r.lease_ticks: a launch lives a
 // bounded time (the server relaunches it at once), so a device-wide synchronisation elsewhere in the server process
@@ -2198,84 +2200,150 @@ constexpr bool kResident = (FAM <= 1 && R <= 8) || (FAM == 2 && R <= 9);
 __device__ __forceinline__ uint32_t ld_sys_u32(const void* p) {
     return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ double ld_sys_f64(const void* p) {
-    const uint64_t v = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+
+__device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the env's next pair from its committed MT19937 state (g: [kMtWords], the read index at g[kN]) at read index idx:
+// words idx .. idx + 3 (normal 2k from words 4k, 4k + 1, normal 2k + 1 from 4k + 2, 4k + 3: k_mt_normals' order);
+// idx >= kN: the 624 words are used up, twisted in the wave's LDS copy mtl (*tw = true; not yet written back).
+// Agent-scope loads: the words the tick path's kernels (other CUs) or this wave's own stores last wrote, past L1.
+__device__ __forceinline__ void resident_pair(const uint32_t* g, uint32_t* mtl, int lane, int idx, bool* tw, double* z0,
+                                              double* z1) {
+    uint32_t w = 0;
+    *tw = idx >= mt::kN;
+    if (*tw) {
+        for (int i = lane; i < mt::kN; i += 64) mtl[i] = ld_agent_u32(g + i);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        mt::twist(mtl, lane);
+        if (lane < 4) w = mtl[lane];
+    } else if (lane < 4) {
+        w = ld_agent_u32(g + idx + lane);
+    }
+    w = mt::temper(w);
+    const uint32_t w1 = (uint32_t)__shfl((int)w, (2 * lane) & 3), w2 = (uint32_t)__shfl((int)w, (2 * lane + 1) & 3);
+    const double x = mt::boxmuller(w1, w2);
+    *z0 = readlane_d(x, 0);
+    *z1 = readlane_d(x, 1);
 }
 
 template <int FAM, int R>
 __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r) {
     __shared__ uint32_t mtl[mt::kN];
+    // the next request's pair, drawn while the client turns round after a served request: valid while the env's
+    // stream epoch is still the served request's (no reseed or tick-path draw since), committed when it is used.
+    // Kept in LDS with the loop's clocks (the step body needs every SGPR it can get: held across the loop, these
+    // values were spilled into VGPR lanes)
+    struct Pf {
+        double z0, z1;
+        uint64_t t_beat, t_end;
+        int32_t idx;        // the committed read index after the served request
+        uint32_t ep;        // the served request's epoch
+        uint32_t beat, count;
+        int32_t state;      // 0 nothing served yet, 1 served (draw ahead), 2 drawn, 3 drawn with a twist (in mtl)
+    };
+    __shared__ Pf pfs;
     const int e = (int)blockIdx.x, lane = (int)threadIdx.x;
     qcs_slot* sl = (qcs_slot*)r.slots + e;
     uint32_t* g = r.mt + (size_t)e * kMtWords;
     uint32_t served = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rdone));
-    uint32_t beat = __builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl + 1));
-    uint64_t t_beat = __builtin_amdgcn_s_memrealtime();
-    const uint64_t t_end = t_beat + r.lease_ticks;
+    if (lane == 0) {
+        pfs.count = ld_sys_u32(&sl->rcount);
+        pfs.beat = ld_sys_u32(r.ctl + 1);
+        pfs.t_beat = __builtin_amdgcn_s_memrealtime();
+        pfs.t_end = pfs.t_beat + r.lease_ticks;
+        pfs.state = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (uint32_t it = 0;; ++it) {
         const uint32_t rq = __builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->rreq));
         if (rq == served) {
+            if (__builtin_amdgcn_readfirstlane(pfs.state) == 1) {   // draw ahead (the state is this wave's commit)
+                bool tw;
+                double z0, z1;
+                resident_pair(g, mtl, lane, __builtin_amdgcn_readfirstlane(pfs.idx), &tw, &z0, &z1);
+                if (lane == 0) {
+                    pfs.z0 = z0;
+                    pfs.z1 = z1;
+                    pfs.state = tw ? 3 : 2;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
             if ((it & 7u) == 0u) {
                 if (__builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl))) break;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(ld_sys_u32(r.ctl + 1));
                 const uint64_t t = __builtin_amdgcn_s_memrealtime();
-                if (b != beat) {
-                    beat = b;
-                    t_beat = t;
-                } else if (t - t_beat > r.beat_ticks) {
-                    break;
+                bool quit = false;
+                if (b != pfs.beat) {
+                    if (lane == 0) {
+                        pfs.beat = b;
+                        pfs.t_beat = t;
+                    }
+                } else if (t - pfs.t_beat > r.beat_ticks) {
+                    quit = true;
                 }
-                if (t > t_end) break;
+                if (t > pfs.t_end) quit = true;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (__builtin_amdgcn_readfirstlane((int)quit)) break;
             }
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
-        // the client's row and request fields (and the tick path's MT19937 writes) are visible from here on
+        // the client's row (and the tick path's MT19937 writes) are visible from here on
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         ResIO io{};
-        io.slot = (int32_t)__builtin_amdgcn_readfirstlane(ld_sys_u32(&sl->ract));
-        const double dt = ld_sys_f64(&sl->dt), gamma = ld_sys_f64(&sl->gamma);
+        io.slot = (int32_t)QCS_RQ_ACT(rq);
+        const uint32_t ep = QCS_RQ_EP(rq);
         int32_t status = 0;
-        if (!(dt == a.dt && gamma == a.gamma) || io.slot < 0 || io.slot >= a.n_slots) {
+        const int pst = __builtin_amdgcn_readfirstlane(pfs.state);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(pfs.count) + 1u;
+        int nst = 0;   // the draw-ahead state after this request (bounced: the client's tick call moves the stream on)
+        if (QCS_RQ_GEN(rq) != r.gen || io.slot >= a.n_slots) {
             status = QCS_EBOUNCE;   // not this kernel's dynamics or action grid: the client takes the tick path
         } else {
-            // the step's pair: words idx .. idx + 3 of the env's stream (normal 2k from words 4k, 4k + 1, normal 2k + 1
-            // from 4k + 2, 4k + 3: k_mt_normals' order), after a twist when the 624 words are used up
-            int idx = (int)__builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(g + mt::kN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            uint32_t w = 0;
-            if (idx >= mt::kN) {
-                for (int i = lane; i < mt::kN; i += 64) mtl[i] = g[i];
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                mt::twist(mtl, lane);
-                for (int i = lane; i < mt::kN; i += 64) g[i] = mtl[i];
-                idx = 0;
-                if (lane < 4) w = mtl[lane];
-            } else if (lane < 4) {
-                w = g[idx + lane];
+            int idx;
+            bool tw;
+            if (pst >= 2 && ep == (uint32_t)__builtin_amdgcn_readfirstlane(pfs.ep)) {
+                // the pair drawn ahead: committed now (with its twist, if it needed one)
+                io.z0 = pfs.z0;
+                io.z1 = pfs.z1;
+                tw = pst == 3;
+                idx = tw ? 0 : __builtin_amdgcn_readfirstlane(pfs.idx);
+            } else {
+                idx = (int)__builtin_amdgcn_readfirstlane(ld_agent_u32(g + mt::kN));
+                resident_pair(g, mtl, lane, idx, &tw, &io.z0, &io.z1);
+                if (tw) idx = 0;
             }
-            w = mt::temper(w);
-            const uint32_t w1 = (uint32_t)__shfl((int)w, (2 * lane) & 3), w2 = (uint32_t)__shfl((int)w, (2 * lane + 1) & 3);
-            const double x = mt::boxmuller(w1, w2);
-            io.z0 = readlane_d(x, 0);
-            io.z1 = readlane_d(x, 1);
-            if (lane == 0) g[mt::kN] = (uint32_t)(idx + 4);
+            if (tw)
+                for (int i = lane; i < mt::kN; i += 64) g[i] = mtl[i];
+            if (lane == 0) {
+                g[mt::kN] = (uint32_t)(idx + 4);
+                pfs.idx = idx + 4;
+                pfs.ep = ep;
+            }
+            nst = 1;
             step_body<FAM, R, 0, double, true, true>(a, nullptr, (uint32_t)e, &io);
         }
         if (lane == 0) {
+            pfs.state = nst;
+            pfs.count = count;
+            pfs.t_beat = __builtin_amdgcn_s_memrealtime();
             sl->q = io.q;
             sl->xmean = io.xm;
             sl->fail = io.fail > 0 ? 1 : 0;
             sl->rstatus = status;
+            sl->rcount = count;
         }
         // the row, the results and the stream's state before rdone (every lane's stores: the fence waits on the wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         if (lane == 0) __hip_atomic_store(&sl->rdone, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         served = rq;
-        t_beat = __builtin_amdgcn_s_memrealtime();
     }
 }
 

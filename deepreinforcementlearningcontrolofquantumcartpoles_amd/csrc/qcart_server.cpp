@@ -44,7 +44,7 @@ namespace qcart {
 void set_global_error(const std::string& m);   // qcart_api.cpp: what qc_last_error(NULL) returns
 bool resident_available(const qc_handle* h);
 int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, double lease_s,
-                    void* stream);
+                    uint32_t gen, void* stream);
 }
 
 namespace {
@@ -122,6 +122,7 @@ struct qc_server {
     // the loop relaunches at once, so a device-wide synchronisation in this process never waits longer
     double lease_us = 20000.0, t_lease = 0;
     int64_t launches = 0;
+    uint32_t r_gen = 0;   // + 1 per dynamics change (dt, gamma): requests checked against older ones bounce
     // MT19937 prefetch (QCART_SERVER_PREFETCH=0 turns it off): after a tick, every owned env that has no drawn pair
     // draws its next step's pair into d_pre (has_pre = 1) while the clients turn round; a 1-step call then steps on
     // it directly and a 10-step call takes it as its step 0 — the normals kernel leaves the tick's critical path.
@@ -189,10 +190,11 @@ void resident_start(qc_server* s) {
     qcs_header* H = s->hdr;
     H->r_dt = s->cur_dt;
     H->r_gamma = s->cur_gamma;
+    __atomic_store_n(&H->r_gen, s->r_gen, __ATOMIC_SEQ_CST);
     __atomic_store_n(&H->r_quit, 0u, __ATOMIC_SEQ_CST);
     const size_t ctl = offsetof(qcs_header, r_quit);
     const int rc = qcart::resident_launch(s->h, s->d_spsi, s->d_shm + H->slot_off, (const uint32_t*)(s->d_shm + ctl),
-                                          1.0, s->lease_us * 1e-6, s->rstream);
+                                          1.0, s->lease_us * 1e-6, s->r_gen, s->rstream);
     if (rc != QC_OK || hipEventRecord(s->r_exit, s->rstream) != hipSuccess) {
         // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0)
         __atomic_store_n(&H->r_on, 0u, __ATOMIC_SEQ_CST);
@@ -301,7 +303,7 @@ void serve_tick(qc_server* s, const std::vector<int>& pend) {
                 resident_stop(s);
                 (void)hipStreamSynchronize(s->stream);
                 rc = qc_set_dynamics(s->h, dt, gamma);
-                if (rc == QC_OK) { s->cur_dt = dt; s->cur_gamma = gamma; }
+                if (rc == QC_OK) { s->cur_dt = dt; s->cur_gamma = gamma; s->r_gen++; }
             }
             int32_t* stb = grp == 0 ? s->st1 : s->st10;
             if (!later.empty()) (void)hipStreamSynchronize(s->stream);   // the budget array is read by the kernels
@@ -694,7 +696,7 @@ int qc_server_timing(const qc_server* s, double* out) {
 int qc_server_resident(const qc_server* s, int64_t* calls, int64_t* launches) {
     if (!s) return QC_EINVAL;
     int64_t n = 0;
-    for (int e = 0; e < s->P; ++e) n += __atomic_load_n(&s->slots[e].rdone, __ATOMIC_ACQUIRE);
+    for (int e = 0; e < s->P; ++e) n += __atomic_load_n(&s->slots[e].rcount, __ATOMIC_ACQUIRE);
     if (calls) *calls = n;
     if (launches) *launches = s->launches;
     return s->resident ? 1 : 0;

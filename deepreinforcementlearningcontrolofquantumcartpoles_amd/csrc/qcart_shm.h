@@ -57,8 +57,9 @@ typedef struct qcs_header {
     /* the resident path (qcart_server.cpp, k_resident): one wave per slot polls the slot's rreq word in this
      * device-mapped object and steps the env in place — no launch, no server thread in the call. r_on: the server
      * has a resident kernel for its module; a client sends step(state, dt, force, gamma) there when dt and gamma
-     * are r_dt / r_gamma and the force is on the action grid (anything else: the tick path) */
-    uint32_t r_on, r_pad0;
+     * are r_dt / r_gamma (read under the generation r_gen, which the request carries) and the force is on the action
+     * grid (anything else: the tick path) */
+    uint32_t r_on, r_gen;
     double r_dt, r_gamma;
     uint64_t r_pad1[8];      /* r_quit / r_beat on a line of their own: the GPU polls it, the clients never read it */
     uint32_t r_quit;         /* set by the server: every resident wave exits */
@@ -80,12 +81,24 @@ typedef struct qcs_slot {
     double q, xmean;         /* step: the last step's q and x_mean */
     double value;            /* x_expectation */
     char err[96];
-    uint32_t rreq;           /* the resident path's request sequence number (client) */
+    uint32_t rreq;           /* the resident request word QCS_RQ(seq, action, gen, epoch) (client): the whole request
+                                in the one word the wave polls */
     uint32_t rdone;          /* = rreq once the resident wave has written the results (device) */
-    int32_t ract;            /* the request's action slot (the force's index on the action grid) */
+    uint32_t repoch;         /* the env's stream epoch: + 1 by the client for every call that takes MT19937 words (or
+                                reseeds) through the ticks, so the wave drops a pair it drew ahead */
     int32_t rstatus;         /* 0, or QCS_EBOUNCE / QCS_EDROPPED */
-    uint8_t pad[16];
+    uint32_t rcount;         /* requests the resident waves have answered for this slot (device; statistics) */
+    uint8_t pad[12];
 } qcs_slot;
+
+/* the resident request word: sequence (12 bits, + 1 per request), the action slot (6 bits, < 64), the generation of
+ * the server's dynamics the client checked (6 bits of r_gen) and the env's stream epoch (8 bits of repoch) */
+#define QCS_RQ(seq, act, gen, ep) \
+    (((uint32_t)(seq) & 0xfffu) | (((uint32_t)(act) & 63u) << 12) | (((uint32_t)(gen) & 63u) << 18) | \
+     (((uint32_t)(ep) & 255u) << 24))
+#define QCS_RQ_ACT(w) (((w) >> 12) & 63u)
+#define QCS_RQ_GEN(w) (((w) >> 18) & 63u)
+#define QCS_RQ_EP(w) ((w) >> 24)
 
 /* inode of this process's PID namespace (0 if /proc is unavailable) */
 static inline uint64_t qcs_pid_ns(void) {

@@ -28,15 +28,15 @@ class Header(ctypes.Structure):
                 ("server_pid", i32), ("slot_off", u64), ("psi_off", u64), ("obs_off", u64), ("total_bytes", u64),
                 ("n_max", i32), ("moment_order", i32), ("omega", d), ("x_max", d), ("grid_size", d), ("lambda_", d),
                 ("mass", d), ("f_max", d), ("n_actions", i32), ("pad1", i32), ("ticks", u64), ("calls", u64),
-                ("pid_ns", u64), ("r_on", u32), ("r_pad0", u32), ("r_dt", d), ("r_gamma", d), ("r_pad1", u64 * 8),
+                ("pid_ns", u64), ("r_on", u32), ("r_gen", u32), ("r_dt", d), ("r_gamma", d), ("r_pad1", u64 * 8),
                 ("r_quit", u32), ("r_beat", u32), ("r_pad2", u64 * 7)]
 
 
 class Slot(ctypes.Structure):
     _fields_ = [("owner", u32), ("pid", i32), ("req", u32), ("done", u32), ("waiting", u32), ("op", i32), ("n", i32),
                 ("seed", u32), ("dt", d), ("force", d), ("gamma", d), ("status", i32), ("fail", i32), ("q", d),
-                ("xmean", d), ("value", d), ("err", ctypes.c_char * 96), ("rreq", u32), ("rdone", u32), ("ract", i32),
-                ("rstatus", i32), ("pad", ctypes.c_uint8 * 16)]
+                ("xmean", d), ("value", d), ("err", ctypes.c_char * 96), ("rreq", u32), ("rdone", u32), ("repoch", u32),
+                ("rstatus", i32), ("rcount", u32), ("pad", ctypes.c_uint8 * 12)]
 
 
 OP_STEP, OP_SET_SEED, OP_X, OP_MOM, OP_FOCK, OP_HDOT = 1, 2, 3, 4, 5, 6
@@ -71,8 +71,9 @@ class MockServer:
     """qcart_server.cpp's side of the protocol in Python: STEP negates the state and reports q = 1.5 n,
     x_mean = force, Fail = n == 10; SET_SEED stores the seed in `value`; X_EXPECT returns the sum of Re(psi);
     MOMENTS fills the obs row with 0, 1, 2, ...; HDOT doubles the row. serve_ops: the ops it answers (others stay
-    pending forever: a server that hangs on them). resident: it also plays the resident kernel (r_on, rreq / rdone:
-    the row times 3, q = 100 + action, x_mean = force, Fail 0), bouncing action `bounce` to the ticks."""
+    pending forever: a server that hangs on them). resident: it also plays the resident kernel (r_on, the request
+    word rreq / rdone: the row times 3, q = 100 + action, x_mean = force, Fail 0), bouncing action `bounce` and
+    requests of another dynamics generation than r_gen to the ticks."""
 
     def __init__(self, name, P=3, N=8, n_obs=5, serve_ops=None, resident=False, bounce=-1):
         self.name, self.P, self.N, self.n_obs = name, P, N, n_obs
@@ -95,6 +96,7 @@ class MockServer:
         h.magic, h.version, h.max_clients, h.N, h.n_obs, h.family = 0x56534351, VERSION, P, N, n_obs, 1
         h.f_max, h.n_actions = 8.0, 21
         self.bounce = bounce
+        self.kernel_gen = None   # the "kernel's" generation (None: the header's)
         if resident:
             h.r_on, h.r_dt, h.r_gamma = 1, 1 / 1440, 6.28
         h.server_pid, h.pid_ns = os.getpid(), os.stat("/proc/self/ns/pid").st_ino
@@ -114,11 +116,14 @@ class MockServer:
             for e in range(self.P):
                 s = self.slots[e]
                 if self.hdr.r_on and s.owner and s.rreq != self.rserved[e]:
-                    if s.ract == self.bounce:
+                    act, gen = (s.rreq >> 12) & 63, (s.rreq >> 18) & 63
+                    kgen = self.hdr.r_gen if self.kernel_gen is None else self.kernel_gen
+                    if act == self.bounce or gen != (kgen & 63):
                         s.rstatus = EBOUNCE
                     else:
                         self.psi[e] *= 3
-                        s.q, s.xmean, s.fail, s.rstatus = 100.0 + s.ract, s.force, 0, 0
+                        s.q, s.xmean, s.fail, s.rstatus = 100.0 + act, s.force, 0, 0
+                    s.rcount += 1
                     self.rserved[e] = s.rreq
                     s.rdone = s.rreq
                     any_ = True
@@ -248,7 +253,20 @@ def test_client_takes_the_resident_path():
         st = base.copy()
         q, xm, fail = a.simulate_10_steps(st, 1 / 1440, 0.8, 6.28)
         assert (q, fail) == (15.0, 1) and np.array_equal(st, -base)
-        assert srv.slots[0].rreq == srv.slots[0].rdone == 3
+        # the request word: sequence 3 so far; every call that took stream words through the ticks (and the open's
+        # set_seed) moved the epoch: 1 + the bounce + 3 + simulate_10_steps = 6
+        s0 = srv.slots[0]
+        assert s0.rreq == s0.rdone and s0.rreq & 0xfff == 3 and s0.repoch == 6 and s0.rcount == 3
+        st = base.copy()
+        a.step(st, 1 / 1440, 1.6, 6.28)
+        assert s0.rreq & 0xfff == 4 and (s0.rreq >> 12) & 63 == 12 and s0.rreq >> 24 == 6
+        srv.kernel_gen = 5                                # a relaunch after a dynamics change: generation 0 bounces
+        st = base.copy()
+        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 1.5 and (s0.rreq >> 18) & 63 == 0
+        srv.hdr.r_gen = 5                                 # ... and the header's: the client's requests carry it
+        st = base.copy()
+        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 112.0 and (s0.rreq >> 18) & 63 == 5
+        del s0
         t0 = time.monotonic()
         a.close()
         assert time.monotonic() - t0 < 1.0 and srv.hdr.n_clients == 0

@@ -366,10 +366,24 @@ int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, d
     KArgs a = base_args(h);
     a.psi = psi;
     a.n_steps = 1;
-    a.tab_mode = 0;
-    a.lds_bytes = 0;
-    a.lds_img = 0;
-    a.lds_nz = 0;
+    // MODE 2 (the request's slot image kept in LDS between requests) for the Fock modules where base_args places the
+    // tables so and every block gets a CU of its own (<= 256 slots; one wave's noise buffer); else MODE 0 (tables from
+    // L2; the grid's MODE 2 body contracts apart from its MODE 0 ticks)
+    // (QCART_RESIDENT_MODE=0 forces the latter, for A/B)
+    static const bool lds_ok = !(std::getenv("QCART_RESIDENT_MODE") && std::atoi(std::getenv("QCART_RESIDENT_MODE")) == 0);
+    if (lds_ok && a.tab_mode == 2 && h->p.batch <= 256 && h->op.fock) {
+        // one slot image per block (not the two-slot layout's), then one wave's noise buffer (base_args' layout)
+        const OpHost& op = h->op;
+        const uint32_t fx = op.fock ? (uint32_t)(op.R + 1 + (op.family == QC_IHO ? op.R : 0)) * kWave * 8u : 0u;
+        a.lds_img = 0;
+        a.lds_nz = (a.lds_fx + fx + 15u) & ~15u;
+        a.lds_bytes = a.lds_nz + kNzLds;
+    } else {
+        a.tab_mode = 0;
+        a.lds_bytes = 0;
+        a.lds_img = 0;
+        a.lds_nz = 0;
+    }
     a.spread = 1;
     a.n_blocks = (uint32_t)h->p.batch;
     a.bad = nullptr;   // the client sends only actions of the grid (anything else bounces to the tick path)

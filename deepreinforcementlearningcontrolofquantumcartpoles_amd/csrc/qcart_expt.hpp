@@ -140,3 +140,10 @@ extern "C" __attribute__((weak)) int qc_debug_stamps(unsigned long long* out) {
 #ifndef QCART_MPIPE_DEPTH
 #define QCART_MPIPE_DEPTH 2
 #endif
+
+// -DQCART_RES_STAMPS (a diagnostic build only, tools/probe_resident_lat.py --stamps): the resident kernel sums, per
+// slot, the s_memrealtime ticks (10 ns) of its request phases — acquire, the pair, the step, the results + release —
+// into the slot's err bytes (unused by the resident path) as 5 uint64: count, then the four sums
+#ifndef QCART_RES_STAMPS
+#define QCART_RES_STAMPS 0
+#endif

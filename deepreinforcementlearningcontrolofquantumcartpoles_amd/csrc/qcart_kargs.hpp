@@ -133,6 +133,7 @@ struct KArgs {
 // the step body takes in registers (RES) instead of through the KArgs arrays
 struct ResIO {
     int32_t slot;               // in: the force slot (the request's action)
+    int32_t reload;             // in: the block's LDS slot image holds another slot (MODE >= 1: copy it again)
     double z0, z1;              // in: the step's two normals (the env's MT19937 stream)
     double q, xm;               // out: the step's q and x_mean
     int32_t fail;               // out: Fail (0 / 1)

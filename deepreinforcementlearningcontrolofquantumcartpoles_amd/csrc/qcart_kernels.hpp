@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // env of this wave: order (envs grouped by force slot, EPB per block, -1 = idle) or identity; a spread MODE 0
     // launch (short calls on small batches, latency-bound) runs one env per block, so that every env has a SIMD
     // (and a CU's L1) to itself instead of sharing one with up to seven others
-    const bool spr = MODE == 0 && a.spread;
+    const bool spr = (MODE == 0 || RES) && a.spread;
     const int64_t e0 = order ? (int64_t)order[blk * EPB] : (spr ? (int64_t)blk : (int64_t)blk * EPB);
     if (e0 < 0 || e0 >= a.B) return;   // whole block idle (uniform over the block)
     // (wave-uniform: made explicit, so every env-derived address lives in SGPRs)
@@ -1279,7 +1279,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // in a row: 17.0 vs 12.1 us per 16-env one-step kernel with everything in device memory
     // (tools/short_call_probe.py). Rows early only where the registers are there (R <= 8 fp64 / 16 fp32: the
     // IHO N = 1024 and grid N = 1025 fallbacks spilled 4 registers each with them)
-    constexpr bool PRE = MODE == 0 && R * sizeof(RT) <= 64;
+    constexpr bool PRE = (MODE == 0 || RES) && R * sizeof(RT) <= 64;
     cx<RT> psi[R];
     int budget0 = 0;
     if constexpr (MODE == 0) {
@@ -1292,6 +1292,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
                     psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
             }
         }
+    } else if constexpr (PRE) {   // RES with the slot image in LDS: the row (host memory) before the image's reload
+        const RT* g0 = (const RT*)a.psi + (size_t)env * a.N * 2;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
     }
     auto clamp_slot = [&](int s) { return s < 0 ? 0 : (s >= a.n_slots ? a.n_slots - 1 : s); };
     // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
@@ -1326,20 +1331,24 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     const double cFd = a.c * a.force[slot];
     const RT cF = (RT)cFd;
     // H_F force coefficients from LDS (apply_hf_fx): fp64 Fock families with the tables in LDS
-    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8;
+    // (not RES: the resident kernel keeps MODE 0's H_F and X^2 arithmetic — its LDS image only moves the factor reads —
+    // so that its steps are bitwise the tick path's and the plain drop-in's short calls, which run MODE 0)
+    constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8 && !RES;
     extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
     char* const simg0 = (char*)smem_dyn;
     char* const simg = simg0 + img_off;   // this wave's slot image (MODE 3: slot A's or slot B's)
     // a block of the no-budget group (k_group puts envs with env_steps <= 0 in whole blocks of their
     // own) takes no step: it skips the table image
     const bool block_idle = order && a.env_steps && (a.env_steps[e0] <= 0 || a.n_steps <= 0);
-    if (MODE >= 1 && !block_idle) {
+    // RES: the image stays in LDS from request to request while the slot does (rio->reload: the slot changed)
+    constexpr uint32_t NTH = RES ? 64u : 64u * (uint32_t)W;   // threads that copy the image
+    if (MODE >= 1 && !block_idle && (!RES || rio->reload)) {
         // the block's slot tables -> LDS once per launch (every thread, 16 B per read), then shared by
         // the 4 waves for all n_steps steps
         char* img = simg0;
         auto copy_from = [&](const rsrc_t& rsrc, uint32_t src, uint32_t dst, uint32_t bytes) {
             if (MODE == 0 || block_idle) return;
-            for (uint32_t o = threadIdx.x * 16u; o < bytes; o += 64u * W * 16u) {
+            for (uint32_t o = threadIdx.x * 16u; o < bytes; o += NTH * 16u) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)o, (int)src, 0);
                 *(uint4*)(img + dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
             }
@@ -1364,7 +1373,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
         }
         static_assert(!(FAM == 2 && MODE == 3 && grid_rows_in_lds(R)), "two-slot blocks carry no row constants");
         if constexpr (FAM == 2 && MODE >= 1 && grid_rows_in_lds(R)) {   // grid row constants (RowLds): hfd, x
-            for (int i = threadIdx.x; i < R * 64; i += 64 * W) {
+            for (int i = threadIdx.x; i < R * 64; i += (int)NTH) {
                 const int j = i >> 6, r = (i & 63) * R + j;
                 const double x = a.xg[r];
                 *(double*)(img + a.lds_fx + i * 8) = (double)((RT)a.hu[r] - cF * (RT)x);
@@ -1498,7 +1507,7 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // the band solve's factor reads run 4 rows ahead in the one-wave-per-SIMD kernels (tables in LDS):
     // C3 186 -> 175 ms, C4 11.5 -> 11.0 ms, C5 53.3 -> 48.6 ms; with two waves per SIMD the partner wave
     // covers the read latency and the deeper reads only cost registers (metric 25.6 -> 25.9 ms)
-    constexpr int SPD = (MODE >= 1 && W == 4) ? 4 : 0;
+    constexpr int SPD = (MODE >= 1 && (W == 4 || RES)) ? 4 : 0;   // (RES: one wave per CU)
     const KArgs& a_in = a;
     // lazy normalisation: psi (and the Fock X psi) are carried unnormalised from step to step — scl is the
     // scale that normalises them, sq = scl^2 (1 before the first step: psi is loaded normalised). The scheme
@@ -2229,7 +2238,10 @@ __device__ __forceinline__ void resident_pair(const uint32_t* g, uint32_t* mtl, 
     *z1 = readlane_d(x, 1);
 }
 
-template <int FAM, int R>
+// MODE 0: the slot tables from L2 on every request; MODE 2 (one block per CU: at most 256 slots): the request's slot
+// image (tables, kept scan composites, H_F force coefficients) stays in LDS while the requests keep the slot (the
+// drivers hold a force for a control interval, 80 steps at the IHO's), copied again when the action changes
+template <int FAM, int R, int MODE>
 __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r) {
     __shared__ uint32_t mtl[mt::kN];
     // the next request's pair, drawn while the client turns round after a served request: valid while the env's
@@ -2243,8 +2255,13 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         uint32_t ep;        // the served request's epoch
         uint32_t beat, count;
         int32_t state;      // 0 nothing served yet, 1 served (draw ahead), 2 drawn, 3 drawn with a twist (in mtl)
+        int32_t img_slot;   // MODE 2: the slot whose image the LDS holds (-1: none)
     };
     __shared__ Pf pfs;
+#if QCART_RES_STAMPS
+    __shared__ uint64_t rst[5];
+    if (threadIdx.x < 5) rst[threadIdx.x] = 0;
+#endif
     const int e = (int)blockIdx.x, lane = (int)threadIdx.x;
     qcs_slot* sl = (qcs_slot*)r.slots + e;
     uint32_t* g = r.mt + (size_t)e * kMtWords;
@@ -2255,6 +2272,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         pfs.t_beat = __builtin_amdgcn_s_memrealtime();
         pfs.t_end = pfs.t_beat + r.lease_ticks;
         pfs.state = 0;
+        pfs.img_slot = -1;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2295,8 +2313,15 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
+#if QCART_RES_STAMPS
+        const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
         // the client's row (and the tick path's MT19937 writes) are visible from here on
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#if QCART_RES_STAMPS
+        const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+        uint64_t ts2 = ts1, ts3 = ts1;
+#endif
         ResIO io{};
         io.slot = (int32_t)QCS_RQ_ACT(rq);
         const uint32_t ep = QCS_RQ_EP(rq);
@@ -2328,7 +2353,18 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
                 pfs.ep = ep;
             }
             nst = 1;
-            step_body<FAM, R, 0, double, true, true>(a, nullptr, (uint32_t)e, &io);
+            if constexpr (MODE >= 1) {
+                io.reload = io.slot != __builtin_amdgcn_readfirstlane(pfs.img_slot);
+                if (lane == 0) pfs.img_slot = io.slot;
+            }
+#if QCART_RES_STAMPS
+            ts2 = __builtin_amdgcn_s_memrealtime();
+#endif
+            step_body<FAM, R, MODE, double, true, true>(a, nullptr, (uint32_t)e, &io);
+#if QCART_RES_STAMPS
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ts3 = __builtin_amdgcn_s_memrealtime();
+#endif
         }
         if (lane == 0) {
             pfs.state = nst;
@@ -2342,6 +2378,17 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         }
         // the row, the results and the stream's state before rdone (every lane's stores: the fence waits on the wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#if QCART_RES_STAMPS
+        if (lane == 0) {
+            const uint64_t ts4 = __builtin_amdgcn_s_memrealtime();
+            rst[0] += 1;
+            rst[1] += ts1 - ts0;
+            rst[2] += ts2 - ts1;
+            rst[3] += ts3 - ts2;
+            rst[4] += ts4 - ts3;
+            for (int i = 0; i < 5; ++i) ((uint64_t*)sl->err)[i] = rst[i];
+        }
+#endif
         if (lane == 0) __hip_atomic_store(&sl->rdone, rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         served = rq;
     }
@@ -2660,7 +2707,21 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
     if (kind == 8) return (kResident<FAM, R> && sizeof(RT) == 8) ? 1 : 0;   // query: a resident kernel
     if (kind == 7) {   // the step server's resident kernel: one 64-lane block per env (slot); `out` is the ResArgs
         if constexpr (kResident<FAM, R> && sizeof(RT) == 8) {
-            hipLaunchKernelGGL((k_resident<FAM, R>), dim3((unsigned)a.B), dim3(64), 0, st, a, *(const ResArgs*)out);
+            // (MODE 2 for the Fock families: the grid TU's cross-statement contraction rounds its MODE 2 body apart
+            // from MODE 0's — IQO x_n = 521 measured — and the grid's resident steps must equal its ticks bitwise)
+            if (FAM <= 1 && a.tab_mode == 2) {
+                static bool attr_set = false;   // > 64 KiB of dynamic LDS
+                if (!attr_set) {
+                    if (hipFuncSetAttribute((const void*)k_resident<FAM, R, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            a.lds_bytes) != hipSuccess)
+                        return -3;
+                    attr_set = true;
+                }
+                hipLaunchKernelGGL((k_resident<FAM, R, 2>), dim3((unsigned)a.B), dim3(64), a.lds_bytes, st, a,
+                                   *(const ResArgs*)out);
+            } else {
+                hipLaunchKernelGGL((k_resident<FAM, R, 0>), dim3((unsigned)a.B), dim3(64), 0, st, a, *(const ResArgs*)out);
+            }
             return hipGetLastError() == hipSuccess ? 0 : -3;
         }
         return -6;

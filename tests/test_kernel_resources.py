@@ -148,13 +148,16 @@ def test_metric_kernel_budget(step_kernels):
     assert v <= 256 and scr <= 12 and sp <= 2 and ssp <= 7
 
 
-# the step server's resident kernels (k_resident<family, R>: the MODE 0 step body inside a polling loop, one wave per
-# slot, fp64: Fock R <= 8, grid R <= 9): no VGPR spills, and SGPR spills at most these ceilings (the loop's own state
-# and the request fields sit beside the step's constants)
-RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)EE")
-RESIDENT_SGPR_SPILLS = {(0, 1): 49, (0, 2): 43, (0, 4): 51, (0, 8): 67,
-                        (1, 1): 59, (1, 2): 51, (1, 3): 55, (1, 4): 59, (1, 8): 75,
-                        (2, 1): 138, (2, 2): 146, (2, 3): 165, (2, 5): 216, (2, 9): 308}
+# the step server's resident kernels (k_resident<family, R, MODE>: the step body inside a polling loop, one wave per
+# slot, fp64: Fock R <= 8, grid R <= 9; MODE 0 tables from L2, MODE 2 the slot image kept in LDS, Fock only): no VGPR spills, and
+# SGPR spills at most these ceilings (the loop's own state and the request sit beside the step's constants)
+RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)ELi(\d+)EE")
+RESIDENT_SGPR_SPILLS = {
+    (0, 1, 0): 49, (0, 1, 2): 35, (0, 2, 0): 43, (0, 2, 2): 41, (0, 4, 0): 51, (0, 4, 2): 57, (0, 8, 0): 67,
+    (0, 8, 2): 59, (1, 1, 0): 59, (1, 1, 2): 59, (1, 2, 0): 51, (1, 2, 2): 41, (1, 3, 0): 55, (1, 3, 2): 43,
+    (1, 4, 0): 59, (1, 4, 2): 47, (1, 8, 0): 75, (1, 8, 2): 61, (2, 1, 0): 138, (2, 1, 2): 126, (2, 2, 0): 146,
+    (2, 2, 2): 136, (2, 3, 0): 165, (2, 3, 2): 156, (2, 5, 0): 216, (2, 5, 2): 196, (2, 9, 0): 308, (2, 9, 2): 254,
+}
 
 
 def test_resident_kernels_budget():
@@ -165,7 +168,7 @@ def test_resident_kernels_budget():
     for name, v, s, scr, sp, ssp in K.kernels(LIB):
         m = RESIDENT.search(name)
         if m:
-            got[(int(m.group(1)), int(m.group(2)))] = (int(v), int(sp), int(ssp))
+            got[(int(m.group(1)), int(m.group(2)), int(m.group(3)))] = (int(v), int(sp), int(ssp))
     assert set(got) == set(RESIDENT_SGPR_SPILLS)
     for k, (v, sp, ssp) in got.items():
         assert v <= 512 and sp == 0 and ssp <= RESIDENT_SGPR_SPILLS[k], (k, v, sp, ssp)

@@ -384,6 +384,9 @@ int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, d
         a.lds_img = 0;
         a.lds_nz = 0;
     }
+    // the block's copy of the row it returned ([Rs][64] complex fp64), after the image and the noise buffer
+    const uint32_t lds_row = a.lds_bytes;
+    a.lds_bytes += (uint32_t)h->op.Rs * kWave * 16u;
     a.spread = 1;
     a.n_blocks = (uint32_t)h->p.batch;
     a.bad = nullptr;   // the client sends only actions of the grid (anything else bounces to the tick path)
@@ -394,6 +397,7 @@ int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, d
     r.beat_ticks = (uint64_t)(beat_s * 1e8);   // s_memrealtime: 100 MHz
     r.lease_ticks = (uint64_t)(lease_s * 1e8);
     r.gen = gen & 63u;
+    r.lds_row = lds_row;
     DeviceGuard g(h->device);
     const int rc = launch_resident(h->p.family, h->op.Rs, a, r, stream);
     return rc ? fail(h, QC_EHIP, "resident kernel launch failed") : QC_OK;

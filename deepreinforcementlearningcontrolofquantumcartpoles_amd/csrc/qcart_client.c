@@ -38,6 +38,7 @@ struct qcc {
     int index;
     double spin_s;   /* how long a call polls its done word before sleeping on the tick word (< 0: adaptive) */
     int cpus;        /* usable host CPUs (affinity mask, capped by the cgroup CPU quota) */
+    int row_kept;    /* the slot's row is the one the resident wave returned last (no call since wrote it) */
     char err[160];
 };
 
@@ -204,11 +205,11 @@ static int grid_action(const qcs_header* h, double force) {
 }
 
 /* post a resident request (the whole request in the rreq word, qcart_shm.h QCS_RQ) and poll for its results */
-static int rcall(qcc* c, int act, uint32_t gen) {
+static int rcall(qcc* c, int act, uint32_t gen, int keep) {
     qcs_slot* s = c->slot;
     qcs_header* h = c->hdr;
     const uint32_t prev = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED);
-    const uint32_t r = QCS_RQ((prev & 0xfffu) + 1u, act, gen, s->repoch);
+    const uint32_t r = QCS_RQ((prev & 0xfffu) + 1u, act, gen, s->repoch, keep);
     __atomic_store_n(&s->rreq, r, __ATOMIC_SEQ_CST);
     /* more clients than usable CPUs: a polling client gives its CPU to the others (sched_yield) */
     const int yield = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) > c->cpus;
@@ -294,7 +295,11 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
              int32_t* fail) {
     if (!c || !psi || (n != 1 && n != 10)) return QCC_EINVAL;
     const size_t bytes = sizeof(double) * 2 * (size_t)c->hdr->N;
-    memcpy(c->psi, psi, bytes);
+    /* keep: the previous call was a resident step and the state still equals the row it returned (the resident wave
+     * then takes its LDS copy of that row instead of reading ours over PCIe) */
+    const int keep = c->row_kept && memcmp(c->psi, psi, bytes) == 0;
+    if (!keep) memcpy(c->psi, psi, bytes);
+    c->row_kept = 0;
     qcs_slot* s = c->slot;
     s->op = QCS_OP_STEP;
     s->n = n;
@@ -308,7 +313,10 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
          * another generation bounces it */
         const uint32_t gen = __atomic_load_n(&h->r_gen, __ATOMIC_ACQUIRE);
         const int act = grid_action(h, force);
-        if (act >= 0 && dt == h->r_dt && gamma == h->r_gamma) rc = rcall(c, act, gen);
+        if (act >= 0 && dt == h->r_dt && gamma == h->r_gamma) {
+            rc = rcall(c, act, gen, keep);
+            if (rc == QCC_OK) c->row_kept = 1;
+        }
     }
     if (rc == QCS_EBOUNCE) {   /* the ticks (a bounced request left the row untouched); they take stream words */
         s->repoch++;
@@ -324,6 +332,7 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
 
 int qcc_set_seed(qcc* c, uint32_t seed) {
     if (!c) return QCC_EINVAL;
+    c->row_kept = 0;
     c->slot->op = QCS_OP_SET_SEED;
     c->slot->seed = seed;
     c->slot->repoch++;   /* a pair the resident wave drew ahead belongs to the old stream */
@@ -332,6 +341,7 @@ int qcc_set_seed(qcc* c, uint32_t seed) {
 
 int qcc_x_expectation(qcc* c, const double* psi, double* out) {
     if (!c || !psi || !out) return QCC_EINVAL;
+    c->row_kept = 0;
     memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
     c->slot->op = QCS_OP_X_EXPECT;
     const int rc = call(c);
@@ -341,6 +351,7 @@ int qcc_x_expectation(qcc* c, const double* psi, double* out) {
 
 int qcc_moments(qcc* c, const double* psi, double* out) {
     if (!c || !psi || !out) return QCC_EINVAL;
+    c->row_kept = 0;
     memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
     c->slot->op = c->hdr->family >= 2 ? QCS_OP_MOMENTS : QCS_OP_FOCK_OBS;
     const int rc = call(c);
@@ -355,6 +366,7 @@ int qcc_hamiltonian_dot_psi(qcc* c, double* psi) {
         return QCC_EINVAL;
     }
     const size_t bytes = sizeof(double) * 2 * (size_t)c->hdr->N;
+    c->row_kept = 0;
     memcpy(c->psi, psi, bytes);
     c->slot->op = QCS_OP_HDOT;
     const int rc = call(c);

@@ -134,6 +134,8 @@ struct KArgs {
 struct ResIO {
     int32_t slot;               // in: the force slot (the request's action)
     int32_t reload;             // in: the block's LDS slot image holds another slot (MODE >= 1: copy it again)
+    int32_t row_lds;            // in: take the row from the block's LDS copy (the one it returned last), not the client's
+    uint32_t lds_row;           // in: byte offset of that copy in the dynamic LDS ([R][64] complex, written every step)
     double z0, z1;              // in: the step's two normals (the env's MT19937 stream)
     double q, xm;               // out: the step's q and x_mean
     int32_t fail;               // out: Fail (0 / 1)
@@ -146,6 +148,7 @@ struct ResArgs {
     uint64_t beat_ticks;        // s_memrealtime ticks (100 MHz) without a heartbeat change before a wave exits
     uint64_t lease_ticks;       // s_memrealtime ticks after which an idle wave exits (the server relaunches the kernel)
     uint32_t gen;               // the server's dynamics generation (6 bits): a request of another one bounces
+    uint32_t lds_row;           // byte offset of the row copy in the dynamic LDS
 };
 int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream);
 bool have_resident(int family, int R);

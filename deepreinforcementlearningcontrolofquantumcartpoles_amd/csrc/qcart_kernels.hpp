@@ -1282,21 +1282,34 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     constexpr bool PRE = (MODE == 0 || RES) && R * sizeof(RT) <= 64;
     cx<RT> psi[R];
     int budget0 = 0;
+    extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
+    // RES: the row from the client's shared-memory row (PCIe), or from the block's LDS copy of the row it returned last
+    auto res_rows = [&]() {
+        if (rio->row_lds) {
+            const cx<RT>* rl = (const cx<RT>*)((const char*)smem_dyn + rio->lds_row);
+#pragma unroll
+            for (int j = 0; j < R; ++j) psi[j] = (gl * R + j < a.N) ? rl[j * 64 + lane] : C(RT(0), RT(0));
+        } else {
+            const RT* g0 = (const RT*)a.psi + (size_t)env * a.N * 2;
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
+        }
+    };
     if constexpr (MODE == 0) {
         if (active) {
             budget0 = a.env_steps ? a.env_steps[env] : a.n_steps;
-            if constexpr (PRE) {
+            if constexpr (PRE && RES) {
+                res_rows();
+            } else if constexpr (PRE) {
                 const RT* g0 = (const RT*)a.psi + (size_t)env * a.N * 2;
 #pragma unroll
                 for (int j = 0; j < R; ++j)
                     psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
             }
         }
-    } else if constexpr (PRE) {   // RES with the slot image in LDS: the row (host memory) before the image's reload
-        const RT* g0 = (const RT*)a.psi + (size_t)env * a.N * 2;
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-            psi[j] = (gl * R + j < a.N) ? ld_cx<RT>(g0 + 2 * (gl * R + j)) : C(RT(0), RT(0));
+    } else if constexpr (PRE) {   // RES with the slot image in LDS: the row before the image's reload
+        res_rows();
     }
     auto clamp_slot = [&](int s) { return s < 0 ? 0 : (s >= a.n_slots ? a.n_slots - 1 : s); };
     // force slot: per wave (MODE 0 and 3), per block (MODE 1, 2: the host groups envs so that every wave of
@@ -1334,7 +1347,6 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // (not RES: the resident kernel keeps MODE 0's H_F and X^2 arithmetic — its LDS image only moves the factor reads —
     // so that its steps are bitwise the tick path's and the plain drop-in's short calls, which run MODE 0)
     constexpr bool FXL = MODE >= 1 && FAM <= 1 && sizeof(RT) == 8 && !RES;
-    extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
     char* const simg0 = (char*)smem_dyn;
     char* const simg = simg0 + img_off;   // this wave's slot image (MODE 3: slot A's or slot B's)
     // a block of the no-budget group (k_group puts envs with env_steps <= 0 in whole blocks of their
@@ -1438,7 +1450,9 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
     // cover its env's lines completely, so the L2 hands HBM whole lines. (Non-temporal 8-B accesses of the real
     // and imaginary halves, round 3's first variant, reached HBM as partial writes: 2.2 GB written per metric
     // launch for 0.54 GB of psi, 4.7 GB at C5, and 1.8x the read bytes)
-    if constexpr (!PRE) {
+    if constexpr (!PRE && RES) {
+        res_rows();
+    } else if constexpr (!PRE) {
 #pragma unroll
         for (int j = 0; j < R; ++j)
             psi[j] = (base + j < N) ? ld_cx<RT>(gpsi + 2 * (base + j)) : C(RT(0), RT(0));
@@ -2138,6 +2152,11 @@ __device__ __forceinline__ void step_body(const KArgs& a, const int32_t* order, 
 #pragma unroll
         for (int j = 0; j < R; ++j)
             if (wb + j < N) st_cx<RT>(gpsi + 2 * (wb + j), psi[j]);
+        if constexpr (RES) {   // the block's copy of the row it returns (taken back when the client keeps it)
+            cx<RT>* rl = (cx<RT>*)((char*)smem_dyn + rio->lds_row);
+#pragma unroll
+            for (int j = 0; j < R; ++j) rl[j * 64 + lane] = psi[j];
+        }
     }
     if constexpr (RES) {
         rio->fail = fail;
@@ -2256,6 +2275,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         uint32_t beat, count;
         int32_t state;      // 0 nothing served yet, 1 served (draw ahead), 2 drawn, 3 drawn with a twist (in mtl)
         int32_t img_slot;   // MODE 2: the slot whose image the LDS holds (-1: none)
+        int32_t row_ok;     // the LDS row copy is the row this launch returned last
     };
     __shared__ Pf pfs;
 #if QCART_RES_STAMPS
@@ -2273,6 +2293,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         pfs.t_end = pfs.t_beat + r.lease_ticks;
         pfs.state = 0;
         pfs.img_slot = -1;
+        pfs.row_ok = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2324,6 +2345,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
 #endif
         ResIO io{};
         io.slot = (int32_t)QCS_RQ_ACT(rq);
+        io.lds_row = r.lds_row;
         const uint32_t ep = QCS_RQ_EP(rq);
         int32_t status = 0;
         const int pst = __builtin_amdgcn_readfirstlane(pfs.state);
@@ -2353,6 +2375,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
                 pfs.ep = ep;
             }
             nst = 1;
+            io.row_lds = QCS_RQ_KEEP(rq) && __builtin_amdgcn_readfirstlane(pfs.row_ok);
             if constexpr (MODE >= 1) {
                 io.reload = io.slot != __builtin_amdgcn_readfirstlane(pfs.img_slot);
                 if (lane == 0) pfs.img_slot = io.slot;
@@ -2368,6 +2391,7 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         }
         if (lane == 0) {
             pfs.state = nst;
+            pfs.row_ok = nst;   // (a bounced request: the client's tick call changes the row)
             pfs.count = count;
             pfs.t_beat = __builtin_amdgcn_s_memrealtime();
             sl->q = io.q;
@@ -2709,18 +2733,24 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
         if constexpr (kResident<FAM, R> && sizeof(RT) == 8) {
             // (MODE 2 for the Fock families: the grid TU's cross-statement contraction rounds its MODE 2 body apart
             // from MODE 0's — IQO x_n = 521 measured — and the grid's resident steps must equal its ticks bitwise)
-            if (FAM <= 1 && a.tab_mode == 2) {
-                static bool attr_set = false;   // > 64 KiB of dynamic LDS
-                if (!attr_set) {
-                    if (hipFuncSetAttribute((const void*)k_resident<FAM, R, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            a.lds_bytes) != hipSuccess)
-                        return -3;
-                    attr_set = true;
+            if (a.tab_mode == 2) {
+                if constexpr (FAM <= 1) {
+                    static bool attr_set = false;   // > 64 KiB of dynamic LDS
+                    if (!attr_set) {
+                        if (hipFuncSetAttribute((const void*)k_resident<FAM, R, 2>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                156 * 1024) != hipSuccess)   // (beside its < 4 KiB of static LDS)
+                            return -3;
+                        attr_set = true;
+                    }
+                    hipLaunchKernelGGL((k_resident<FAM, R, 2>), dim3((unsigned)a.B), dim3(64), a.lds_bytes, st, a,
+                                       *(const ResArgs*)out);
+                } else {
+                    return -6;
                 }
-                hipLaunchKernelGGL((k_resident<FAM, R, 2>), dim3((unsigned)a.B), dim3(64), a.lds_bytes, st, a,
-                                   *(const ResArgs*)out);
             } else {
-                hipLaunchKernelGGL((k_resident<FAM, R, 0>), dim3((unsigned)a.B), dim3(64), 0, st, a, *(const ResArgs*)out);
+                hipLaunchKernelGGL((k_resident<FAM, R, 0>), dim3((unsigned)a.B), dim3(64), a.lds_bytes, st, a,
+                                   *(const ResArgs*)out);
             }
             return hipGetLastError() == hipSuccess ? 0 : -3;
         }

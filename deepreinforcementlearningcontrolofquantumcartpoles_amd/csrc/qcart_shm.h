@@ -92,13 +92,16 @@ typedef struct qcs_slot {
 } qcs_slot;
 
 /* the resident request word: sequence (12 bits, + 1 per request), the action slot (6 bits, < 64), the generation of
- * the server's dynamics the client checked (6 bits of r_gen) and the env's stream epoch (8 bits of repoch) */
-#define QCS_RQ(seq, act, gen, ep) \
+ * the server's dynamics the client checked (6 bits of r_gen), the env's stream epoch (7 bits of repoch) and `keep`:
+ * the row is the one the wave returned last (the client's previous call was a resident step and its state array still
+ * equals that row), so the wave may take it from its LDS copy instead of reading it over PCIe */
+#define QCS_RQ(seq, act, gen, ep, keep) \
     (((uint32_t)(seq) & 0xfffu) | (((uint32_t)(act) & 63u) << 12) | (((uint32_t)(gen) & 63u) << 18) | \
-     (((uint32_t)(ep) & 255u) << 24))
+     (((uint32_t)(ep) & 127u) << 24) | ((uint32_t)((keep) ? 1u : 0u) << 31))
 #define QCS_RQ_ACT(w) (((w) >> 12) & 63u)
 #define QCS_RQ_GEN(w) (((w) >> 18) & 63u)
-#define QCS_RQ_EP(w) ((w) >> 24)
+#define QCS_RQ_EP(w) (((w) >> 24) & 127u)
+#define QCS_RQ_KEEP(w) ((w) >> 31)
 
 /* inode of this process's PID namespace (0 if /proc is unavailable) */
 static inline uint64_t qcs_pid_ns(void) {

@@ -109,6 +109,8 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
         st[0] = 1.0
         qs = []
         for k in range(steps):
+            if k == 120:
+                st *= -1j          # the driver changes the state between calls (the resident wave reads it again)
             qs.append(plain.step(st, dt, 0.8 * ((k // 80 + c) % 3 - 1), gamma))
         want.append((st.copy(), qs, plain.x_expectation(st)))
     name = _name()
@@ -124,6 +126,8 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
             st[0] = 1.0
             qs = []
             for k in range(steps):
+                if k == 120:
+                    st *= -1j
                 qs.append(m.step(st, dt, 0.8 * ((k // 80 + c) % 3 - 1), gamma))
             got[c] = (st.copy(), qs, m.x_expectation(st))
             m.close()

@@ -153,10 +153,10 @@ def test_metric_kernel_budget(step_kernels):
 # SGPR spills at most these ceilings (the loop's own state and the request sit beside the step's constants)
 RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)ELi(\d+)EE")
 RESIDENT_SGPR_SPILLS = {
-    (0, 1, 0): 49, (0, 1, 2): 35, (0, 2, 0): 43, (0, 2, 2): 41, (0, 4, 0): 51, (0, 4, 2): 57, (0, 8, 0): 67,
-    (0, 8, 2): 59, (1, 1, 0): 59, (1, 1, 2): 59, (1, 2, 0): 51, (1, 2, 2): 41, (1, 3, 0): 55, (1, 3, 2): 43,
-    (1, 4, 0): 59, (1, 4, 2): 47, (1, 8, 0): 75, (1, 8, 2): 61, (2, 1, 0): 138, (2, 1, 2): 126, (2, 2, 0): 146,
-    (2, 2, 2): 136, (2, 3, 0): 165, (2, 3, 2): 156, (2, 5, 0): 216, (2, 5, 2): 196, (2, 9, 0): 308, (2, 9, 2): 254,
+    (0, 1, 0): 49, (0, 1, 2): 37, (0, 2, 0): 43, (0, 2, 2): 36, (0, 4, 0): 57, (0, 4, 2): 61, (0, 8, 0): 67,
+    (0, 8, 2): 56, (1, 1, 0): 60, (1, 1, 2): 60, (1, 2, 0): 51, (1, 2, 2): 35, (1, 3, 0): 55, (1, 3, 2): 41,
+    (1, 4, 0): 59, (1, 4, 2): 45, (1, 8, 0): 75, (1, 8, 2): 61, (2, 1, 0): 136, (2, 2, 0): 148, (2, 3, 0): 166,
+    (2, 5, 0): 216, (2, 9, 0): 307,
 }
 
 

@@ -240,6 +240,12 @@ def test_client_takes_the_resident_path():
         st = base.copy()
         q, xm, fail = a.step(st, 1 / 1440, 0.8, 6.28)            # grid action 11 (spacing 0.8): resident
         assert (q, xm, fail) == (111.0, 0.8, 0) and np.array_equal(st, 3 * base)
+        assert srv.slots[0].rreq >> 31 == 0                      # the first call: the row read from the slot
+        a.step(st, 1 / 1440, 0.8, 6.28)                          # the state as returned: `keep`
+        assert srv.slots[0].rreq >> 31 == 1 and np.array_equal(st, 9 * base)
+        st[0] += 1                                               # changed by the driver: read again
+        a.step(st, 1 / 1440, 0.8, 6.28)
+        assert srv.slots[0].rreq >> 31 == 0
         st = base.copy()
         q, xm, fail = a.step(st, 1 / 1440, -8.0, 6.28)           # action 0
         assert q == 100.0 and np.array_equal(st, 3 * base)
@@ -253,13 +259,13 @@ def test_client_takes_the_resident_path():
         st = base.copy()
         q, xm, fail = a.simulate_10_steps(st, 1 / 1440, 0.8, 6.28)
         assert (q, fail) == (15.0, 1) and np.array_equal(st, -base)
-        # the request word: sequence 3 so far; every call that took stream words through the ticks (and the open's
+        # the request word: sequence 5 so far; every call that took stream words through the ticks (and the open's
         # set_seed) moved the epoch: 1 + the bounce + 3 + simulate_10_steps = 6
         s0 = srv.slots[0]
-        assert s0.rreq == s0.rdone and s0.rreq & 0xfff == 3 and s0.repoch == 6 and s0.rcount == 3
+        assert s0.rreq == s0.rdone and s0.rreq & 0xfff == 5 and s0.repoch == 6 and s0.rcount == 5
         st = base.copy()
         a.step(st, 1 / 1440, 1.6, 6.28)
-        assert s0.rreq & 0xfff == 4 and (s0.rreq >> 12) & 63 == 12 and s0.rreq >> 24 == 6
+        assert s0.rreq & 0xfff == 6 and (s0.rreq >> 12) & 63 == 12 and (s0.rreq >> 24) & 127 == 6
         srv.kernel_gen = 5                                # a relaunch after a dynamics change: generation 0 bounces
         st = base.copy()
         assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 1.5 and (s0.rreq >> 18) & 63 == 0

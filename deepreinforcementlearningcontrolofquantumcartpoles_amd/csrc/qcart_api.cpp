@@ -370,7 +370,8 @@ int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, d
     // tables so and every block gets a CU of its own (<= 256 slots; one wave's noise buffer); else MODE 0 (tables from
     // L2; the grid's MODE 2 body contracts apart from its MODE 0 ticks)
     // (QCART_RESIDENT_MODE=0 forces the latter, for A/B)
-    static const bool lds_ok = !(std::getenv("QCART_RESIDENT_MODE") && std::atoi(std::getenv("QCART_RESIDENT_MODE")) == 0);
+    const char* rm = std::getenv("QCART_RESIDENT_MODE");   // (read per launch: a launch lives a 20 ms lease)
+    const bool lds_ok = !(rm && std::atoi(rm) == 0);
     if (lds_ok && a.tab_mode == 2 && h->p.batch <= 256 && h->op.fock) {
         // one slot image per block (not the two-slot layout's), then one wave's noise buffer (base_args' layout)
         const OpHost& op = h->op;

@@ -87,16 +87,19 @@ def test_served_simulate_10_steps_matches_oracle(served, oracle_mod):
     TN.test_dropin_simulate_10_steps_matches_oracle(oracle_mod)
 
 
-@pytest.mark.parametrize("mode", ["resident", "short_lease", "ticks"])
+@pytest.mark.parametrize("mode", ["resident", "short_lease", "l2_tables", "ticks"])
 def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
     """Four clients on one server, each in its own thread (the ctypes calls release the GIL), each its own seed and
     forces: every state bitwise equal to the plain drop-in's run of the same sequence, and the x_expectation served
     in the same ticks. resident: the step calls go to the resident kernel (one wave per slot polling the shared
-    object); short_lease: each launch lives 0.3 ms, so the calls straddle many relaunches; ticks
+    object); short_lease: each launch lives 0.3 ms, so the calls straddle many relaunches; l2_tables: the resident
+    kernel reading the slot tables from L2 on every request (its MODE 0, the one beyond 256 slots); ticks
     (QCART_SERVER_RESIDENT=0): every call is batched into the ticks."""
     resident = mode != "ticks"
     if not resident:
         monkeypatch.setenv("QCART_SERVER_RESIDENT", "0")
+    if mode == "l2_tables":
+        monkeypatch.setenv("QCART_RESIDENT_MODE", "0")
     if mode == "short_lease":
         monkeypatch.setenv("QCART_RESIDENT_LEASE_MS", "0.3")
     n_max, P, steps = 180, 4, 240

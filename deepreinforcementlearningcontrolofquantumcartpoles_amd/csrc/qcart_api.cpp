@@ -38,8 +38,8 @@ namespace qcart {
 void set_global_error(const std::string& m) { set_create_err(m); }
 // the step server's resident kernel (qcart_server.cpp): declared here, defined after qc_handle
 bool resident_available(const qc_handle* h);
-int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, double lease_s,
-                    uint32_t gen, void* stream);
+int resident_launch(qc_handle* h, void* psi, void* slots, double* obs, const uint32_t* ctl, double beat_s,
+                    double lease_s, uint32_t gen, void* stream);
 }  // namespace qcart
 
 struct qc_handle {
@@ -360,8 +360,8 @@ bool resident_available(const qc_handle* h) {
 }
 // k_resident over the handle's B envs (env e = slot e): the KArgs of qc_step's short one-step call (MODE 0, one env
 // per block, no grouping) — the same step body and constants, so both paths step an env bitwise alike
-int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, double lease_s,
-                    uint32_t gen, void* stream) {
+int resident_launch(qc_handle* h, void* psi, void* slots, double* obs, const uint32_t* ctl, double beat_s,
+                    double lease_s, uint32_t gen, void* stream) {
     if (!resident_available(h)) return fail(h, QC_EINVAL, "no resident kernel for this module");
     KArgs a = base_args(h);
     a.psi = psi;
@@ -399,6 +399,7 @@ int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, d
     r.lease_ticks = (uint64_t)(lease_s * 1e8);
     r.gen = gen & 63u;
     r.lds_row = lds_row;
+    r.obs = obs;
     DeviceGuard g(h->device);
     const int rc = launch_resident(h->p.family, h->op.Rs, a, r, stream);
     return rc ? fail(h, QC_EHIP, "resident kernel launch failed") : QC_OK;

@@ -205,11 +205,11 @@ static int grid_action(const qcs_header* h, double force) {
 }
 
 /* post a resident request (the whole request in the rreq word, qcart_shm.h QCS_RQ) and poll for its results */
-static int rcall(qcc* c, int act, uint32_t gen, int keep) {
+static int rcall(qcc* c, int op, int act, uint32_t gen, int keep) {
     qcs_slot* s = c->slot;
     qcs_header* h = c->hdr;
     const uint32_t prev = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED);
-    const uint32_t r = QCS_RQ((prev & 0xfffu) + 1u, act, gen, s->repoch, keep);
+    const uint32_t r = QCS_RQ((prev & 0x3ffu) + 1u, op, act, gen, s->repoch, keep);
     __atomic_store_n(&s->rreq, r, __ATOMIC_SEQ_CST);
     /* more clients than usable CPUs: a polling client gives its CPU to the others (sched_yield) */
     const int yield = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) > c->cpus;
@@ -314,7 +314,7 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
         const uint32_t gen = __atomic_load_n(&h->r_gen, __ATOMIC_ACQUIRE);
         const int act = grid_action(h, force);
         if (act >= 0 && dt == h->r_dt && gamma == h->r_gamma) {
-            rc = rcall(c, act, gen, keep);
+            rc = rcall(c, QCS_ROP_STEP, act, gen, keep);
             if (rc == QCC_OK) c->row_kept = 1;
         }
     }
@@ -339,22 +339,33 @@ int qcc_set_seed(qcc* c, uint32_t seed) {
     return call(c);
 }
 
+/* x_expectation / the observation vector: on the resident kernel when the server has one (the stream and the row the
+ * wave keeps stay as they are: a kept row stays kept), else in a tick */
+static int obs_call(qcc* c, const double* psi, int rop, int op) {
+    const size_t bytes = sizeof(double) * 2 * (size_t)c->hdr->N;
+    const int keep = c->row_kept && memcmp(c->psi, psi, bytes) == 0;
+    if (!keep) memcpy(c->psi, psi, bytes);
+    c->row_kept = keep;
+    /* (the grid's resident kernel bounces them: its moments stay in the ticks) */
+    if (__atomic_load_n(&c->hdr->r_on, __ATOMIC_ACQUIRE) && c->hdr->family <= 1) {
+        const int rc = rcall(c, rop, 0, 0u, keep);
+        if (rc != QCS_EBOUNCE) return rc;
+    }
+    c->row_kept = 0;
+    c->slot->op = op;
+    return call(c);
+}
+
 int qcc_x_expectation(qcc* c, const double* psi, double* out) {
     if (!c || !psi || !out) return QCC_EINVAL;
-    c->row_kept = 0;
-    memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
-    c->slot->op = QCS_OP_X_EXPECT;
-    const int rc = call(c);
+    const int rc = obs_call(c, psi, QCS_ROP_X_EXPECT, QCS_OP_X_EXPECT);
     if (rc == QCC_OK) *out = c->slot->value;
     return rc;
 }
 
 int qcc_moments(qcc* c, const double* psi, double* out) {
     if (!c || !psi || !out) return QCC_EINVAL;
-    c->row_kept = 0;
-    memcpy(c->psi, psi, sizeof(double) * 2 * (size_t)c->hdr->N);
-    c->slot->op = c->hdr->family >= 2 ? QCS_OP_MOMENTS : QCS_OP_FOCK_OBS;
-    const int rc = call(c);
+    const int rc = obs_call(c, psi, QCS_ROP_OBS, c->hdr->family >= 2 ? QCS_OP_MOMENTS : QCS_OP_FOCK_OBS);
     if (rc == QCC_OK) memcpy(out, c->obs, sizeof(double) * (size_t)c->hdr->n_obs);
     return rc;
 }

@@ -149,6 +149,7 @@ struct ResArgs {
     uint64_t lease_ticks;       // s_memrealtime ticks after which an idle wave exits (the server relaunches the kernel)
     uint32_t gen;               // the server's dynamics generation (6 bits): a request of another one bounces
     uint32_t lds_row;           // byte offset of the row copy in the dynamic LDS
+    double* obs;                // device address of the shm object's obs rows ([B][QCS_MAX_OBS])
 };
 int launch_resident(int family, int R, const KArgs& a, const ResArgs& r, void* stream);
 bool have_resident(int family, int R);

@@ -2260,6 +2260,55 @@ __device__ __forceinline__ void resident_pair(const uint32_t* g, uint32_t* mtl, 
 // MODE 0: the slot tables from L2 on every request; MODE 2 (one block per CU: at most 256 slots): the request's slot
 // image (tables, kept scan composites, H_F force coefficients) stays in LDS while the requests keep the slot (the
 // drivers hold a force for a control interval, 80 steps at the IHO's), copied again when the action changes
+// x_expectation / the observation vector of the block's env on the resident path: k_aux's what = 0 and k_obs's code on
+// the same row (bitwise their results), the row from the client's slot or the block's LDS copy (row_lds)
+template <int FAM, int R>
+__device__ __forceinline__ void resident_obs(const KArgs& a, const ResArgs& r, qcs_slot* sl, int e, int lane, uint32_t op,
+                                             bool row_lds) {
+    extern __shared__ __attribute__((aligned(16))) double smem_dyn[];
+    const int base = lane * R, N = a.N;
+    Coef<FAM, R> cf;
+    load_coef<FAM, R>(cf, a, base);
+    cd psi[R];
+    if (row_lds) {
+        const cd* rl = (const cd*)((const char*)smem_dyn + r.lds_row);
+#pragma unroll
+        for (int j = 0; j < R; ++j) psi[j] = (base + j < N) ? rl[j * 64 + lane] : C(0.0, 0.0);
+    } else {
+        const size_t e0 = (size_t)e * N;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double* q = (const double*)a.psi + 2 * (e0 + base + j);   // (ld_psi<double>'s two loads)
+            psi[j] = (base + j < N) ? C(q[0], q[1]) : C(0.0, 0.0);
+        }
+    }
+    if (op == QCS_ROP_X_EXPECT) {
+        double s[3] = {0.0, 0.0, 0.0};
+        cd xp[R];
+        apply_x<FAM, R>(psi, xp, cf, lane);
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[0] += psi[j].re * xp[j].re + psi[j].im * xp[j].im;
+        wave_sum<3>(s);
+        if (lane == 0) sl->value = s[0] * a.w;
+    } else {
+        double* orow = r.obs + (size_t)e * QCS_MAX_OBS;
+        if constexpr (FAM <= 1) {
+            double o[5];
+            fock_obs<FAM, R>(psi, cf, lane, o);
+            if (lane < 5) {
+                double v = o[0];
+#pragma unroll
+                for (int i = 1; i < 5; ++i) v = (lane == i) ? o[i] : v;
+                orow[lane] = v;
+            }
+        } else {
+            auto xm = [&]() { return RowReg<R>{cf.xg, cf.xg}; };
+            const double v = grid_obs<kMaxMoment, R>(psi, cf, xm, lane, a.moment_order, a.h);
+            if (lane < a.n_obs) orow[lane] = v;
+        }
+    }
+}
+
 template <int FAM, int R, int MODE>
 __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r) {
     __shared__ uint32_t mtl[mt::kN];
@@ -2349,9 +2398,20 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         const uint32_t ep = QCS_RQ_EP(rq);
         int32_t status = 0;
         const int pst = __builtin_amdgcn_readfirstlane(pfs.state);
+        const int prow = __builtin_amdgcn_readfirstlane(pfs.row_ok);
         const uint32_t count = __builtin_amdgcn_readfirstlane(pfs.count) + 1u;
+        const uint32_t op = QCS_RQ_OP(rq);
         int nst = 0;   // the draw-ahead state after this request (bounced: the client's tick call moves the stream on)
-        if (QCS_RQ_GEN(rq) != r.gen || io.slot >= a.n_slots) {
+        int nrow = 0;  // the LDS row copy after this request
+        if (op != QCS_ROP_STEP) {
+            // x_expectation / observations (Fock modules: the grid's moments up to order 9 beside the step body cost
+            // its kernel ~50 more spilled SGPRs, so they bounce to the ticks): the stream, the drawn pair and the row
+            // copy stay as they are
+            if constexpr (FAM <= 1) resident_obs<FAM, R>(a, r, sl, e, lane, op, QCS_RQ_KEEP(rq) && prow);
+            else status = QCS_EBOUNCE;
+            nst = pst;
+            nrow = prow;
+        } else if (QCS_RQ_GEN(rq) != r.gen || io.slot >= a.n_slots) {
             status = QCS_EBOUNCE;   // not this kernel's dynamics or action grid: the client takes the tick path
         } else {
             int idx;
@@ -2375,7 +2435,8 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
                 pfs.ep = ep;
             }
             nst = 1;
-            io.row_lds = QCS_RQ_KEEP(rq) && __builtin_amdgcn_readfirstlane(pfs.row_ok);
+            nrow = 1;
+            io.row_lds = QCS_RQ_KEEP(rq) && prow;
             if constexpr (MODE >= 1) {
                 io.reload = io.slot != __builtin_amdgcn_readfirstlane(pfs.img_slot);
                 if (lane == 0) pfs.img_slot = io.slot;
@@ -2391,12 +2452,14 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         }
         if (lane == 0) {
             pfs.state = nst;
-            pfs.row_ok = nst;   // (a bounced request: the client's tick call changes the row)
+            pfs.row_ok = nrow;   // (a bounced request: the client's tick call changes the row)
             pfs.count = count;
             pfs.t_beat = __builtin_amdgcn_s_memrealtime();
-            sl->q = io.q;
-            sl->xmean = io.xm;
-            sl->fail = io.fail > 0 ? 1 : 0;
+            if (op == QCS_ROP_STEP) {
+                sl->q = io.q;
+                sl->xmean = io.xm;
+                sl->fail = io.fail > 0 ? 1 : 0;
+            }
             sl->rstatus = status;
             sl->rcount = count;
         }

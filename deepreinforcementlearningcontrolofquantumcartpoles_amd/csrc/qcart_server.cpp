@@ -43,8 +43,8 @@
 namespace qcart {
 void set_global_error(const std::string& m);   // qcart_api.cpp: what qc_last_error(NULL) returns
 bool resident_available(const qc_handle* h);
-int resident_launch(qc_handle* h, void* psi, void* slots, const uint32_t* ctl, double beat_s, double lease_s,
-                    uint32_t gen, void* stream);
+int resident_launch(qc_handle* h, void* psi, void* slots, double* obs, const uint32_t* ctl, double beat_s,
+                    double lease_s, uint32_t gen, void* stream);
 }
 
 namespace {
@@ -193,8 +193,9 @@ void resident_start(qc_server* s) {
     __atomic_store_n(&H->r_gen, s->r_gen, __ATOMIC_SEQ_CST);
     __atomic_store_n(&H->r_quit, 0u, __ATOMIC_SEQ_CST);
     const size_t ctl = offsetof(qcs_header, r_quit);
-    const int rc = qcart::resident_launch(s->h, s->d_spsi, s->d_shm + H->slot_off, (const uint32_t*)(s->d_shm + ctl),
-                                          1.0, s->lease_us * 1e-6, s->r_gen, s->rstream);
+    const int rc = qcart::resident_launch(s->h, s->d_spsi, s->d_shm + H->slot_off, (double*)(s->d_shm + H->obs_off),
+                                          (const uint32_t*)(s->d_shm + ctl), 1.0, s->lease_us * 1e-6, s->r_gen,
+                                          s->rstream);
     if (rc != QC_OK || hipEventRecord(s->r_exit, s->rstream) != hipSuccess) {
         // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0)
         __atomic_store_n(&H->r_on, 0u, __ATOMIC_SEQ_CST);

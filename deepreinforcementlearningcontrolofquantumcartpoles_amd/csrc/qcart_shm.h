@@ -81,8 +81,8 @@ typedef struct qcs_slot {
     double q, xmean;         /* step: the last step's q and x_mean */
     double value;            /* x_expectation */
     char err[96];
-    uint32_t rreq;           /* the resident request word QCS_RQ(seq, action, gen, epoch) (client): the whole request
-                                in the one word the wave polls */
+    uint32_t rreq;           /* the resident request word QCS_RQ(seq, op, action, gen, epoch, keep) (client): the whole
+                                request in the one word the wave polls */
     uint32_t rdone;          /* = rreq once the resident wave has written the results (device) */
     uint32_t repoch;         /* the env's stream epoch: + 1 by the client for every call that takes MT19937 words (or
                                 reseeds) through the ticks, so the wave drops a pair it drew ahead */
@@ -91,13 +91,19 @@ typedef struct qcs_slot {
     uint8_t pad[12];
 } qcs_slot;
 
-/* the resident request word: sequence (12 bits, + 1 per request), the action slot (6 bits, < 64), the generation of
- * the server's dynamics the client checked (6 bits of r_gen), the env's stream epoch (7 bits of repoch) and `keep`:
- * the row is the one the wave returned last (the client's previous call was a resident step and its state array still
- * equals that row), so the wave may take it from its LDS copy instead of reading it over PCIe */
-#define QCS_RQ(seq, act, gen, ep, keep) \
-    (((uint32_t)(seq) & 0xfffu) | (((uint32_t)(act) & 63u) << 12) | (((uint32_t)(gen) & 63u) << 18) | \
-     (((uint32_t)(ep) & 127u) << 24) | ((uint32_t)((keep) ? 1u : 0u) << 31))
+/* the resident request word: sequence (10 bits, + 1 per request), the op (2 bits: QCS_ROP_*), the action slot (6 bits,
+ * < 64), the generation of the server's dynamics the client checked (6 bits of r_gen), the env's stream epoch (7 bits
+ * of repoch) and `keep`: the row is the one the wave returned last (the client's previous call was a resident step and
+ * its state array still equals that row), so the wave may take it from its LDS copy instead of reading it over PCIe */
+enum qcs_rop {
+    QCS_ROP_STEP = 0,        /* step(state, dt, force, gamma) */
+    QCS_ROP_X_EXPECT = 1,    /* x_expectation(state) -> value */
+    QCS_ROP_OBS = 2          /* get_moments (grid) / the Fock 'xp' 5-vector -> the slot's obs row */
+};
+#define QCS_RQ(seq, op, act, gen, ep, keep) \
+    (((uint32_t)(seq) & 0x3ffu) | (((uint32_t)(op) & 3u) << 10) | (((uint32_t)(act) & 63u) << 12) | \
+     (((uint32_t)(gen) & 63u) << 18) | (((uint32_t)(ep) & 127u) << 24) | ((uint32_t)((keep) ? 1u : 0u) << 31))
+#define QCS_RQ_OP(w) (((w) >> 10) & 3u)
 #define QCS_RQ_ACT(w) (((w) >> 12) & 63u)
 #define QCS_RQ_GEN(w) (((w) >> 18) & 63u)
 #define QCS_RQ_EP(w) (((w) >> 24) & 127u)

@@ -115,7 +115,9 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
             if k == 120:
                 st *= -1j          # the driver changes the state between calls (the resident wave reads it again)
             qs.append(plain.step(st, dt, 0.8 * ((k // 80 + c) % 3 - 1), gamma))
-        want.append((st.copy(), qs, plain.x_expectation(st)))
+        obs = np.zeros(5)
+        plain._impl.get_moments(st, obs)   # the Fock 'xp' 5-vector (IHO/main_parallel.py:129-131)
+        want.append((st.copy(), qs, plain.x_expectation(st), tuple(obs)))
     name = _name()
     srv = S.StepServer(cfg.IHO, max_clients=P, name=name, n_max=n_max).start()
     got = [None] * P
@@ -132,7 +134,9 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
                 if k == 120:
                     st *= -1j
                 qs.append(m.step(st, dt, 0.8 * ((k // 80 + c) % 3 - 1), gamma))
-            got[c] = (st.copy(), qs, m.x_expectation(st))
+            obs = np.zeros(5)
+            m.get_moments(st, obs)
+            got[c] = (st.copy(), qs, m.x_expectation(st), tuple(obs))
             m.close()
         except Exception as e:   # reported below
             errs.append(repr(e))
@@ -146,13 +150,14 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
         assert np.array_equal(got[c][0], want[c][0]), c
         assert got[c][1] == want[c][1], c
         assert got[c][2] == want[c][2], c
+        assert got[c][3] == want[c][3], c
     assert stats["resident"] == resident
-    if resident:                                      # the steps on the resident kernel, the rest in ticks
-        assert stats["resident_calls"] == P * steps and stats["calls"] == P * 3
+    if resident:   # the steps, the observations and x_expectation on the resident kernel, the set_seed calls in ticks
+        assert stats["resident_calls"] == P * (steps + 2) and stats["calls"] == P * 2
         if mode == "short_lease":
             assert stats["resident_launches"] >= 10, stats
     else:
-        assert stats["calls"] == P * (steps + 3)      # set_seed(0) at open, set_seed, steps, x_expectation
+        assert stats["calls"] == P * (steps + 4)      # set_seed(0) at open, set_seed, steps, observations, x_expectation
         assert stats["ticks"] < stats["calls"]        # ticks served several envs at once
 
 

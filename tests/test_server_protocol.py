@@ -72,8 +72,9 @@ class MockServer:
     x_mean = force, Fail = n == 10; SET_SEED stores the seed in `value`; X_EXPECT returns the sum of Re(psi);
     MOMENTS fills the obs row with 0, 1, 2, ...; HDOT doubles the row. serve_ops: the ops it answers (others stay
     pending forever: a server that hangs on them). resident: it also plays the resident kernel (r_on, the request
-    word rreq / rdone: the row times 3, q = 100 + action, x_mean = force, Fail 0), bouncing action `bounce` and
-    requests of another dynamics generation than r_gen to the ticks."""
+    word rreq / rdone: a step multiplies the row by 3, q = 100 + action, x_mean = force, Fail 0; x_expectation returns
+    minus the sum of Re(psi); the observation row 100, 101, ...), bouncing action `bounce` and steps of another
+    dynamics generation than r_gen to the ticks."""
 
     def __init__(self, name, P=3, N=8, n_obs=5, serve_ops=None, resident=False, bounce=-1):
         self.name, self.P, self.N, self.n_obs = name, P, N, n_obs
@@ -116,9 +117,14 @@ class MockServer:
             for e in range(self.P):
                 s = self.slots[e]
                 if self.hdr.r_on and s.owner and s.rreq != self.rserved[e]:
-                    act, gen = (s.rreq >> 12) & 63, (s.rreq >> 18) & 63
+                    op, act, gen = (s.rreq >> 10) & 3, (s.rreq >> 12) & 63, (s.rreq >> 18) & 63
                     kgen = self.hdr.r_gen if self.kernel_gen is None else self.kernel_gen
-                    if act == self.bounce or gen != (kgen & 63):
+                    if op == 1:
+                        s.value, s.rstatus = -float(self.psi[e].real.sum()), 0
+                    elif op == 2:
+                        self.obs[e, :self.n_obs] = 100 + np.arange(self.n_obs)
+                        s.rstatus = 0
+                    elif act == self.bounce or gen != (kgen & 63):
                         s.rstatus = EBOUNCE
                     else:
                         self.psi[e] *= 3
@@ -262,10 +268,15 @@ def test_client_takes_the_resident_path():
         # the request word: sequence 5 so far; every call that took stream words through the ticks (and the open's
         # set_seed) moved the epoch: 1 + the bounce + 3 + simulate_10_steps = 6
         s0 = srv.slots[0]
-        assert s0.rreq == s0.rdone and s0.rreq & 0xfff == 5 and s0.repoch == 6 and s0.rcount == 5
+        assert s0.rreq == s0.rdone and s0.rreq & 0x3ff == 5 and s0.repoch == 6 and s0.rcount == 5
         st = base.copy()
         a.step(st, 1 / 1440, 1.6, 6.28)
-        assert s0.rreq & 0xfff == 6 and (s0.rreq >> 12) & 63 == 12 and (s0.rreq >> 24) & 127 == 6
+        assert s0.rreq & 0x3ff == 6 and (s0.rreq >> 12) & 63 == 12 and (s0.rreq >> 24) & 127 == 6
+        # x_expectation and the observation vector on the resident path too (op bits 10-11), the stream untouched
+        assert a.x_expectation(st) == -float(st.real.sum()) and (s0.rreq >> 10) & 3 == 1 and s0.repoch == 6
+        data = np.zeros(5)
+        a.get_moments(st, data)
+        assert np.array_equal(data, 100 + np.arange(5.0)) and (s0.rreq >> 10) & 3 == 2
         srv.kernel_gen = 5                                # a relaunch after a dynamics change: generation 0 bounces
         st = base.copy()
         assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 1.5 and (s0.rreq >> 18) & 63 == 0

@@ -496,3 +496,20 @@ def test_server_name_collision_and_stale_objects():
     finally:
         if os.path.exists("/dev/shm" + name2):
             os.unlink("/dev/shm" + name2)
+
+
+def test_soak_mixed_calls_from_processes_bitwise(tmp_path):
+    """tools/soak_server.py at a small size: 4 actor processes, each a random mix of 300 calls (grid and off-grid steps,
+    simulate_10_steps, set_seed, x_expectation, observations, Hamiltonian_dot_psi, driver-side resets) through one
+    server, every return and state digest replayed bitwise on the plain drop-in."""
+    import json
+    import subprocess
+    import sys
+    out = tmp_path / "soak.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "soak_server.py"), "--procs", "4", "--calls", "300",
+                        "--n-max", "63", "--out", str(out)], cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    row = json.load(open(out))
+    assert row["mismatches"] == 0 and row["calls"] == 4 * 301
+    assert row["server"]["resident"] and row["server"]["resident_calls"] > 4 * 200
+

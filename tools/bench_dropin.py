@@ -66,6 +66,9 @@ def worker(args):
 
         def step(F):
             return sim.step(state, dt, F, gamma)
+
+        def xexp():
+            return sim.x_expectation(state)
     else:
         from oracle import oracle as O
         o = O.OracleSystem(O.IHO, n_max=args.n_max, omega=pi)
@@ -73,6 +76,9 @@ def worker(args):
 
         def step(F):
             return o.step(state, dt, F, gamma, mt.normals(2))
+
+        def xexp():
+            return o.x_expectation(state)
     for k in range(200):                              # warm-up (tables of the forces used below)
         step(0.8 * ((k // 80) % 3 - 1))
         if k % 80 == 79:
@@ -89,6 +95,8 @@ def worker(args):
         for _ in range(80):                            # one control interval per force
             step(0.8 * ((n // 80) % 3 - 1))
             n += 1
+        if args.driver_loop:                           # the IHO driver's termination test per control interval
+            xexp()
         state[:] = 0                                   # restart the episode (keeps the env physical)
         state[0] = 1.0
         t = time.time()
@@ -145,7 +153,7 @@ def fan_out(args, kind, P):
     errs = [open(go + f".err{r}", "w+") for r in range(P)]
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker", "--kind", kind, "--rank", str(r),
                                "--go", go, "--seconds", str(args.seconds), "--n-max", str(args.n_max),
-                               "--name", name],
+                               "--name", name] + (["--driver-loop"] if args.driver_loop else []),
                               cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=errs[r], text=True)
              for r in range(P)]
 
@@ -183,7 +191,8 @@ def fan_out(args, kind, P):
         t, n = np.array(r["marks"]).T
         inside += float(np.interp(T1, t, n) - np.interp(T0, t, n))
     agg = inside / (T1 - T0)
-    row = {"kind": kind, "procs": P, "step_calls_per_s": agg, "per_proc_calls_per_s": agg / P,
+    row = {"kind": kind, "procs": P, "driver_loop": bool(args.driver_loop), "step_calls_per_s": agg,
+           "per_proc_calls_per_s": agg / P,
            "us_per_call": P / agg * 1e6, "seconds": args.seconds, "common_window_s": T1 - T0}
     if cs0 and cs1:
         row["cgroup"] = {k: cs1[k] - cs0.get(k, 0) for k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")
@@ -209,6 +218,8 @@ def main():
     ap.add_argument("--name", default="")
     ap.add_argument("--max-clients", type=int, default=16)
     ap.add_argument("--batch-wait-us", type=float, default=40.0)
+    ap.add_argument("--driver-loop", action="store_true",
+                    help="also x_expectation once per 80-step control interval (IHO/main_parallel.py:246), as the driver")
     ap.add_argument("--server-prof", default="", help="run the server under rocprofv3 kernel + HIP trace into DIR")
     args = ap.parse_args()
     if args.serve:

@@ -39,10 +39,13 @@ struct qcc {
     double spin_s;   /* how long a call polls its done word before sleeping on the tick word (< 0: adaptive) */
     int cpus;        /* usable host CPUs (affinity mask, capped by the cgroup CPU quota) */
     int row_kept;    /* the slot's row is the one the resident wave returned last (no call since wrote it) */
+    uint32_t last_rep;   /* the stream epoch this client's last resident step carried */
     char err[160];
 };
 
 static char g_err[160];
+
+static int rcall(qcc* c, int op, int act, uint32_t gen, int keep);
 
 static void set_err(qcc* c, const char* m) {
     snprintf(c ? c->err : g_err, sizeof(g_err), "%s", m);
@@ -144,6 +147,16 @@ int qcc_open(const char* name, qcc** out) {
     c->obs = (double*)(m + h->obs_off) + (size_t)idx * QCS_MAX_OBS;
     c->slot->pid = (int32_t)getpid();
     __atomic_add_fetch(&h->n_clients, 1u, __ATOMIC_SEQ_CST);
+    c->last_rep = c->slot->repoch;
+    if (__atomic_load_n(&h->r_on, __ATOMIC_ACQUIRE)) {
+        /* what the resident wave holds for this slot (a pair drawn ahead, a kept row) is the previous owner's */
+        const int rc = rcall(c, QCS_ROP_RESET, 0, 0u, 0);
+        if (rc && rc != QCS_EBOUNCE) {   /* (the grid kernels answer every non-step op with a bounce) */
+            snprintf(g_err, sizeof(g_err), "%s", c->err);
+            qcc_close(c);
+            return rc;
+        }
+    }
     /* the env starts on seed 0's stream, whatever an earlier owner of the slot left (the plain drop-in's state
      * before the first set_seed) */
     const int rc = qcc_set_seed(c, 0u);
@@ -209,7 +222,9 @@ static int rcall(qcc* c, int op, int act, uint32_t gen, int keep) {
     qcs_slot* s = c->slot;
     qcs_header* h = c->hdr;
     const uint32_t prev = __atomic_load_n(&s->rreq, __ATOMIC_RELAXED);
-    const uint32_t r = QCS_RQ((prev & 0x3ffu) + 1u, op, act, gen, s->repoch, keep);
+    if (op == QCS_ROP_STEP && s->repoch != c->last_rep && ((s->repoch - c->last_rep) & QCS_RQ_EP_MASK) == 0)
+        s->repoch++;   /* tick-path draws since the last resident step must show in the word's 15 epoch bits */
+    const uint32_t r = QCS_RQ((prev & 3u) + 1u, op, act, gen, s->repoch, keep);
     __atomic_store_n(&s->rreq, r, __ATOMIC_SEQ_CST);
     /* more clients than usable CPUs: a polling client gives its CPU to the others (sched_yield) */
     const int yield = (int)__atomic_load_n(&h->n_clients, __ATOMIC_RELAXED) > c->cpus;
@@ -315,7 +330,10 @@ int qcc_step(qcc* c, double* psi, int32_t n, double dt, double force, double gam
         const int act = grid_action(h, force);
         if (act >= 0 && dt == h->r_dt && gamma == h->r_gamma) {
             rc = rcall(c, QCS_ROP_STEP, act, gen, keep);
-            if (rc == QCC_OK) c->row_kept = 1;
+            if (rc == QCC_OK) {
+                c->row_kept = 1;
+                c->last_rep = s->repoch;
+            }
         }
     }
     if (rc == QCS_EBOUNCE) {   /* the ticks (a bounced request left the row untouched); they take stream words */

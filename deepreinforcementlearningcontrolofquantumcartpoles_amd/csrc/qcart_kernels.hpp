@@ -2406,11 +2406,13 @@ __global__ __launch_bounds__(64) void k_resident(const KArgs a, const ResArgs r)
         if (op != QCS_ROP_STEP) {
             // x_expectation / observations (Fock modules: the grid's moments up to order 9 beside the step body cost
             // its kernel ~50 more spilled SGPRs, so they bounce to the ticks): the stream, the drawn pair and the row
-            // copy stay as they are
+            // copy stay as they are; a reset (a new owner of the slot) drops the last two (it also runs the
+            // observation path on whatever row the slot holds, result unread: a guard around the call costs the Fock
+            // kernels ~40 more spilled SGPRs)
             if constexpr (FAM <= 1) resident_obs<FAM, R>(a, r, sl, e, lane, op, QCS_RQ_KEEP(rq) && prow);
             else status = QCS_EBOUNCE;
-            nst = pst;
-            nrow = prow;
+            nst = op == QCS_ROP_RESET ? 0 : pst;
+            nrow = op == QCS_ROP_RESET ? 0 : prow;
         } else if (QCS_RQ_GEN(rq) != r.gen || io.slot >= a.n_slots) {
             status = QCS_EBOUNCE;   // not this kernel's dynamics or action grid: the client takes the tick path
         } else {

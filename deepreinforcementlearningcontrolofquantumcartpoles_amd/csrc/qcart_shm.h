@@ -91,22 +91,26 @@ typedef struct qcs_slot {
     uint8_t pad[12];
 } qcs_slot;
 
-/* the resident request word: sequence (10 bits, + 1 per request), the op (2 bits: QCS_ROP_*), the action slot (6 bits,
- * < 64), the generation of the server's dynamics the client checked (6 bits of r_gen), the env's stream epoch (7 bits
- * of repoch) and `keep`: the row is the one the wave returned last (the client's previous call was a resident step and
- * its state array still equals that row), so the wave may take it from its LDS copy instead of reading it over PCIe */
+/* the resident request word: a sequence (2 bits, + 1 per request: a word only has to differ from the one served
+ * before it), the op (2 bits: QCS_ROP_*), the action slot (6 bits, < 64), the generation of the server's dynamics the
+ * client checked (6 bits of r_gen), the env's stream epoch (15 bits of repoch; the client never lets two of its resident
+ * steps carry equal epochs across tick-path draws, and a new owner of the slot first sends QCS_ROP_RESET) and `keep`:
+ * the row is the one the wave returned last (the client's previous call was a resident step and its state array still
+ * equals that row), so the wave may take it from its LDS copy instead of reading it over PCIe */
 enum qcs_rop {
     QCS_ROP_STEP = 0,        /* step(state, dt, force, gamma) */
     QCS_ROP_X_EXPECT = 1,    /* x_expectation(state) -> value */
-    QCS_ROP_OBS = 2          /* get_moments (grid) / the Fock 'xp' 5-vector -> the slot's obs row */
+    QCS_ROP_OBS = 2,         /* get_moments (grid) / the Fock 'xp' 5-vector -> the slot's obs row */
+    QCS_ROP_RESET = 3        /* a new owner: the wave drops the pair it drew ahead and the row it kept */
 };
 #define QCS_RQ(seq, op, act, gen, ep, keep) \
-    (((uint32_t)(seq) & 0x3ffu) | (((uint32_t)(op) & 3u) << 10) | (((uint32_t)(act) & 63u) << 12) | \
-     (((uint32_t)(gen) & 63u) << 18) | (((uint32_t)(ep) & 127u) << 24) | ((uint32_t)((keep) ? 1u : 0u) << 31))
-#define QCS_RQ_OP(w) (((w) >> 10) & 3u)
-#define QCS_RQ_ACT(w) (((w) >> 12) & 63u)
-#define QCS_RQ_GEN(w) (((w) >> 18) & 63u)
-#define QCS_RQ_EP(w) (((w) >> 24) & 127u)
+    (((uint32_t)(seq) & 3u) | (((uint32_t)(op) & 3u) << 2) | (((uint32_t)(act) & 63u) << 4) | \
+     (((uint32_t)(gen) & 63u) << 10) | (((uint32_t)(ep) & 0x7fffu) << 16) | ((uint32_t)((keep) ? 1u : 0u) << 31))
+#define QCS_RQ_EP_MASK 0x7fffu
+#define QCS_RQ_OP(w) (((w) >> 2) & 3u)
+#define QCS_RQ_ACT(w) (((w) >> 4) & 63u)
+#define QCS_RQ_GEN(w) (((w) >> 10) & 63u)
+#define QCS_RQ_EP(w) (((w) >> 16) & QCS_RQ_EP_MASK)
 #define QCS_RQ_KEEP(w) ((w) >> 31)
 
 /* inode of this process's PID namespace (0 if /proc is unavailable) */

@@ -154,9 +154,9 @@ def test_metric_kernel_budget(step_kernels):
 RESIDENT = re.compile(r"k_residentILi(\d+)ELi(\d+)ELi(\d+)EE")
 RESIDENT_SGPR_SPILLS = {
     (0, 1, 0): 51, (0, 1, 2): 39, (0, 2, 0): 45, (0, 2, 2): 39, (0, 4, 0): 59, (0, 4, 2): 59, (0, 8, 0): 69,
-    (0, 8, 2): 57, (1, 1, 0): 61, (1, 1, 2): 63, (1, 2, 0): 53, (1, 2, 2): 39, (1, 3, 0): 57, (1, 3, 2): 43,
+    (0, 8, 2): 59, (1, 1, 0): 61, (1, 1, 2): 63, (1, 2, 0): 53, (1, 2, 2): 39, (1, 3, 0): 57, (1, 3, 2): 43,
     (1, 4, 0): 61, (1, 4, 2): 47, (1, 8, 0): 77, (1, 8, 2): 63, (2, 1, 0): 136, (2, 2, 0): 146, (2, 3, 0): 170,
-    (2, 5, 0): 219, (2, 9, 0): 287,
+    (2, 5, 0): 219, (2, 9, 0): 291,
 }
 
 

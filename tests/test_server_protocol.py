@@ -45,6 +45,11 @@ VERSION = 3
 EBOUNCE = -101
 
 
+def rq_fields(w):
+    """The resident request word (qcart_shm.h QCS_RQ): seq, op, action, generation, epoch, keep."""
+    return w & 3, (w >> 2) & 3, (w >> 4) & 63, (w >> 10) & 63, (w >> 16) & 0x7fff, w >> 31
+
+
 def test_layout_mirror_matches_the_c_header(tmp_path):
     if shutil.which("gcc") is None:
         pytest.skip("no gcc")
@@ -117,9 +122,11 @@ class MockServer:
             for e in range(self.P):
                 s = self.slots[e]
                 if self.hdr.r_on and s.owner and s.rreq != self.rserved[e]:
-                    op, act, gen = (s.rreq >> 10) & 3, (s.rreq >> 12) & 63, (s.rreq >> 18) & 63
+                    _, op, act, gen, _, _ = rq_fields(s.rreq)
                     kgen = self.hdr.r_gen if self.kernel_gen is None else self.kernel_gen
-                    if op == 1:
+                    if op == 3:
+                        s.rstatus = 0
+                    elif op == 1:
                         s.value, s.rstatus = -float(self.psi[e].real.sum()), 0
                     elif op == 2:
                         self.obs[e, :self.n_obs] = 100 + np.arange(self.n_obs)
@@ -246,12 +253,12 @@ def test_client_takes_the_resident_path():
         st = base.copy()
         q, xm, fail = a.step(st, 1 / 1440, 0.8, 6.28)            # grid action 11 (spacing 0.8): resident
         assert (q, xm, fail) == (111.0, 0.8, 0) and np.array_equal(st, 3 * base)
-        assert srv.slots[0].rreq >> 31 == 0                      # the first call: the row read from the slot
+        assert rq_fields(srv.slots[0].rreq)[5] == 0              # the first call: the row read from the slot
         a.step(st, 1 / 1440, 0.8, 6.28)                          # the state as returned: `keep`
-        assert srv.slots[0].rreq >> 31 == 1 and np.array_equal(st, 9 * base)
+        assert rq_fields(srv.slots[0].rreq)[5] == 1 and np.array_equal(st, 9 * base)
         st[0] += 1                                               # changed by the driver: read again
         a.step(st, 1 / 1440, 0.8, 6.28)
-        assert srv.slots[0].rreq >> 31 == 0
+        assert rq_fields(srv.slots[0].rreq)[5] == 0
         st = base.copy()
         q, xm, fail = a.step(st, 1 / 1440, -8.0, 6.28)           # action 0
         assert q == 100.0 and np.array_equal(st, 3 * base)
@@ -265,24 +272,32 @@ def test_client_takes_the_resident_path():
         st = base.copy()
         q, xm, fail = a.simulate_10_steps(st, 1 / 1440, 0.8, 6.28)
         assert (q, fail) == (15.0, 1) and np.array_equal(st, -base)
-        # the request word: sequence 5 so far; every call that took stream words through the ticks (and the open's
-        # set_seed) moved the epoch: 1 + the bounce + 3 + simulate_10_steps = 6
+        # the resident requests so far: the open's reset and 5 steps; every call that took stream words through the
+        # ticks (and the open's set_seed) moved the epoch: 1 + the bounce + 3 + simulate_10_steps = 6
         s0 = srv.slots[0]
-        assert s0.rreq == s0.rdone and s0.rreq & 0x3ff == 5 and s0.repoch == 6 and s0.rcount == 5
+        assert s0.rreq == s0.rdone and s0.repoch == 6 and s0.rcount == 6
         st = base.copy()
         a.step(st, 1 / 1440, 1.6, 6.28)
-        assert s0.rreq & 0x3ff == 6 and (s0.rreq >> 12) & 63 == 12 and (s0.rreq >> 24) & 127 == 6
-        # x_expectation and the observation vector on the resident path too (op bits 10-11), the stream untouched
-        assert a.x_expectation(st) == -float(st.real.sum()) and (s0.rreq >> 10) & 3 == 1 and s0.repoch == 6
+        _, op, act, gen, ep, keep = rq_fields(s0.rreq)
+        assert (op, act, gen, ep, keep) == (0, 12, 0, 6, 0)
+        # x_expectation and the observation vector on the resident path too (op 1, 2), the stream untouched
+        assert a.x_expectation(st) == -float(st.real.sum()) and rq_fields(s0.rreq)[1] == 1 and s0.repoch == 6
         data = np.zeros(5)
         a.get_moments(st, data)
-        assert np.array_equal(data, 100 + np.arange(5.0)) and (s0.rreq >> 10) & 3 == 2
+        assert np.array_equal(data, 100 + np.arange(5.0)) and rq_fields(s0.rreq)[1] == 2
+        # 2^15 tick-path draws since the last resident step would alias in the word's 15 epoch bits: the client moves
+        # the epoch on once more
+        last = rq_fields(s0.rreq)[4]
+        s0.repoch += 0x8000
+        st = base.copy()
+        a.step(st, 1 / 1440, 1.6, 6.28)
+        assert rq_fields(s0.rreq)[4] == (last + 1) & 0x7fff and s0.repoch == 6 + 0x8000 + 1
         srv.kernel_gen = 5                                # a relaunch after a dynamics change: generation 0 bounces
         st = base.copy()
-        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 1.5 and (s0.rreq >> 18) & 63 == 0
+        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 1.5 and rq_fields(s0.rreq)[3] == 0
         srv.hdr.r_gen = 5                                 # ... and the header's: the client's requests carry it
         st = base.copy()
-        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 112.0 and (s0.rreq >> 18) & 63 == 5
+        assert a.step(st, 1 / 1440, 1.6, 6.28)[0] == 112.0 and rq_fields(s0.rreq)[3] == 5
         del s0
         t0 = time.monotonic()
         a.close()

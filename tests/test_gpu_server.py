@@ -152,8 +152,9 @@ def test_concurrent_clients_equal_the_plain_dropin(monkeypatch, mode):
         assert got[c][2] == want[c][2], c
         assert got[c][3] == want[c][3], c
     assert stats["resident"] == resident
-    if resident:   # the steps, the observations and x_expectation on the resident kernel, the set_seed calls in ticks
-        assert stats["resident_calls"] == P * (steps + 2) and stats["calls"] == P * 2
+    if resident:   # the steps, the observations, x_expectation and the reset at open on the resident kernel, the
+        # set_seed calls in ticks
+        assert stats["resident_calls"] == P * (steps + 3) and stats["calls"] == P * 2
         if mode == "short_lease":
             assert stats["resident_launches"] >= 10, stats
     else:
@@ -304,7 +305,7 @@ def test_grid_clients_equal_the_plain_dropin(family):
     for c in range(P):
         assert np.array_equal(got[c][0], want[c][0]), c
         assert got[c][1] == want[c][1], c
-    assert stats["resident"] and stats["resident_calls"] == P * 120, stats
+    assert stats["resident"] and stats["resident_calls"] == P * 121, stats   # (the steps and the reset at open)
 
 
 def test_device_synchronize_in_the_server_process_returns():

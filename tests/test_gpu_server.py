@@ -259,6 +259,42 @@ def test_resident_kernel_survives_table_changes_bitwise():
     assert stats["resident"] and stats["resident_calls"] >= P * 80, stats
 
 
+def test_resident_epoch_does_not_alias_after_2_15_reseeds(monkeypatch):
+    """The request word carries 15 bits of the env's stream epoch. A client that reseeds exactly 2^15 times between two
+    resident steps brings the epoch back to the same 15 bits: without the client's alias guard the wave would take the
+    pair it drew ahead from the old stream. States and returns must stay bitwise the plain drop-in's (which reseeds once:
+    the stream is the same), and the steps on both sides of the reseeds must be resident ones — of ONE launch (a 10 s
+    lease: a relaunch would drop the drawn pair and hide the alias; with the guard disabled this test fails)."""
+    monkeypatch.setenv("QCART_RESIDENT_LEASE_MS", "10000")
+    n_max, dt, gamma = 180, 1 / 1440, 2 * pi
+
+    def calls(m, reseeds):
+        m.set_seed(11)
+        st = np.zeros(n_max + 1, np.complex128)
+        st[0] = 1.0
+        out = [tuple(m.step(st, dt, 0.8, gamma)) for _ in range(3)]
+        for _ in range(reseeds):
+            m.set_seed(12)
+        out += [tuple(m.step(st, dt, -0.8, gamma)) for _ in range(3)]
+        return st.copy(), out
+
+    want = calls(S.load(cfg.IHO, n_max=n_max), 1)
+    name = _name()
+    srv = S.StepServer(cfg.IHO, max_clients=1, name=name, n_max=n_max).start()
+    try:
+        m = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=n_max), name)
+        got = calls(m, 1 << 15)
+        m.close()
+        stats = srv.stats()
+    finally:
+        srv.close()
+    assert np.array_equal(got[0], want[0])
+    assert got[1] == want[1]
+    # the reset at open and the six steps on the resident kernel; the reseeds in ticks
+    assert stats["resident"] and stats["resident_calls"] == 7 and stats["calls"] == 2 + (1 << 15), stats
+    assert stats["resident_launches"] == 1, stats
+
+
 def _grid_calls(m, c, ph, gamma):
     """A grid driver's calls: set_seed, steps at action-grid forces (the resident kernel), get_moments every 20th."""
     m.set_seed(700 + c)

@@ -13,8 +13,13 @@ own `simulation` module stepping one env): P independent processes, each `instal
           one batched launch
   cpu     the oracle (the CPU restatement, one env and one host core each — what the reference's processes do)
 The aggregate counts every process's step calls inside the COMMON window [latest start, earliest end] (each
-process records its call count after every 80-step control interval; counts at the window edges interpolated)
-divided by that window. The parent never touches the GPU; each process is a fresh child.
+process records its call count after every control interval; counts at the window edges interpolated) divided by
+that window. The parent never touches the GPU; each process is a fresh child.
+
+--family (default inverted_harmonic): any of the four modules at its driver defaults (config.DEFAULTS; --n-max for the
+Fock ones): dt, gamma and the action grid's forces of that driver, one control interval per force (IHO 80 steps, IQO
+160), the episode restarted after each from |0> (Fock) or the drivers' Gaussian packet (grid). --driver-loop adds the
+driver's per-interval call: x_expectation (IHO/main_parallel.py:246) or get_moments (IQO/main_parallel.py:134,202).
 """
 import argparse
 import json
@@ -52,38 +57,62 @@ def single(args):
     print(json.dumps({"n_max": args.n_max, **out}))
 
 
+def physics(args):
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    fam = {v: k for k, v in cfg.FAMILY_NAMES.items()}[args.family]
+    ph = cfg.DEFAULTS[fam]
+    return ph.with_(n_max=args.n_max) if ph.fock else ph
+
+
+def initial_state(ph):
+    """|0> (Fock) or the grid drivers' Gaussian packet (mean 0, std 1, IQO/main_parallel.py:182-183)."""
+    if ph.fock:
+        st = np.zeros(ph.dim, np.complex128)
+        st[0] = 1.0
+        return st
+    x = (np.arange(ph.dim) - ph.dim // 2) * ph.grid_size
+    st = np.exp(-x * x / 4.0).astype(np.complex128)
+    return st / np.linalg.norm(st)
+
+
 def worker(args):
-    """One actor process: the drivers' call sequence (install, set_seed, step per dt; force redrawn every 80
-    steps) on one env, timed after the go file appears."""
-    dt, gamma = 1 / 1440, 2 * pi
-    state = np.zeros(args.n_max + 1, np.complex128)
-    state[0] = 1.0
+    """One actor process: the drivers' call sequence (install, set_seed, step per dt; a force of the action grid per
+    control interval) on one env, timed after the go file appears."""
+    ph = physics(args)
+    dt, gamma, ci = ph.dt, ph.gamma, ph.control_interval
+    half = ph.n_actions // 2
+    state = initial_state(ph)
+    fresh = state.copy()
+    obs = np.zeros(ph.n_obs)
     if args.kind in ("gpu", "server"):
         from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
-        sim = S.install("inverted_harmonic", device=0, n_max=args.n_max,
-                        server=args.name if args.kind == "server" else None)
+        kw = {"n_max": args.n_max} if ph.fock else {}
+        sim = S.install(args.family, device=0, server=args.name if args.kind == "server" else None, **kw)
         sim.set_seed(1000 + args.rank)
 
         def step(F):
             return sim.step(state, dt, F, gamma)
 
-        def xexp():
-            return sim.x_expectation(state)
+        def per_interval():
+            return sim.x_expectation(state) if ph.fock else sim.get_moments(state, obs)
     else:
         from oracle import oracle as O
-        o = O.OracleSystem(O.IHO, n_max=args.n_max, omega=pi)
+        o = O.OracleSystem(ph.family, n_max=ph.n_max, omega=ph.omega, x_max=ph.x_max, grid_size=ph.grid_size,
+                           lambda_=ph.lambda_, mass=ph.mass, moment_order=ph.moment_order)
         mt = O.MT19937(1000 + args.rank)
 
         def step(F):
             return o.step(state, dt, F, gamma, mt.normals(2))
 
-        def xexp():
-            return o.x_expectation(state)
-    for k in range(200):                              # warm-up (tables of the forces used below)
-        step(0.8 * ((k // 80) % 3 - 1))
-        if k % 80 == 79:
-            state[:] = 0
-            state[0] = 1.0
+        def per_interval():
+            return o.x_expectation(state) if ph.fock else o.moments(state)
+
+    def force(n):
+        return ph.force(half + (n // ci) % 3 - 1)
+    for k in range(3 * ci):                          # warm-up (tables of the forces used below)
+        step(force(k))
+        if k % ci == ci - 1:
+            state[:] = fresh
     print("ready", flush=True)
     while not os.path.exists(args.go):
         time.sleep(0.001)
@@ -92,13 +121,12 @@ def worker(args):
     t_end = t0 + args.seconds
     marks = [(t0, 0)]
     while True:
-        for _ in range(80):                            # one control interval per force
-            step(0.8 * ((n // 80) % 3 - 1))
+        for _ in range(ci):                            # one control interval per force
+            step(force(n))
             n += 1
-        if args.driver_loop:                           # the IHO driver's termination test per control interval
-            xexp()
-        state[:] = 0                                   # restart the episode (keeps the env physical)
-        state[0] = 1.0
+        if args.driver_loop:                           # the driver's own call per control interval
+            per_interval()
+        state[:] = fresh                               # restart the episode (keeps the env physical)
         t = time.time()
         marks.append((t, n))
         if t >= t_end:
@@ -110,8 +138,9 @@ def serve(args):
     """The step-server process: owns the GPU, serves until its stdin closes, prints its statistics."""
     import threading
     from deepreinforcementlearningcontrolofquantumcartpoles_amd import simulation as S
-    srv = S.StepServer("inverted_harmonic", max_clients=args.max_clients, name=args.name, device=0,
-                       batch_wait_us=args.batch_wait_us, n_max=args.n_max)
+    kw = {"n_max": args.n_max} if physics(args).fock else {}
+    srv = S.StepServer(args.family, max_clients=args.max_clients, name=args.name, device=0,
+                       batch_wait_us=args.batch_wait_us, **kw)
 
     def watch():
         sys.stdin.read()
@@ -140,7 +169,7 @@ def fan_out(args, kind, P):
     if kind == "server":
         serr = open(go + ".server_err", "w+")
         cmd = [sys.executable, os.path.abspath(__file__), "--serve", "--name", name, "--max-clients", str(P),
-               "--n-max", str(args.n_max), "--batch-wait-us", str(args.batch_wait_us)]
+               "--n-max", str(args.n_max), "--batch-wait-us", str(args.batch_wait_us), "--family", args.family]
         if args.server_prof:   # the server under rocprofv3 (kernel + HIP API trace: tools/server_timeline.py)
             cmd = ["rocprofv3", "--kernel-trace", "--hip-trace", "--output-format", "csv", "-d",
                    os.path.abspath(args.server_prof), "-o", "run", "--"] + cmd
@@ -153,7 +182,7 @@ def fan_out(args, kind, P):
     errs = [open(go + f".err{r}", "w+") for r in range(P)]
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker", "--kind", kind, "--rank", str(r),
                                "--go", go, "--seconds", str(args.seconds), "--n-max", str(args.n_max),
-                               "--name", name] + (["--driver-loop"] if args.driver_loop else []),
+                               "--name", name, "--family", args.family] + (["--driver-loop"] if args.driver_loop else []),
                               cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=errs[r], text=True)
              for r in range(P)]
 
@@ -218,8 +247,10 @@ def main():
     ap.add_argument("--name", default="")
     ap.add_argument("--max-clients", type=int, default=16)
     ap.add_argument("--batch-wait-us", type=float, default=40.0)
+    ap.add_argument("--family", default="inverted_harmonic", help="harmonic / inverted_harmonic / quartic / inverted_quartic")
     ap.add_argument("--driver-loop", action="store_true",
-                    help="also x_expectation once per 80-step control interval (IHO/main_parallel.py:246), as the driver")
+                    help="also the driver's per-interval call: x_expectation (IHO/main_parallel.py:246) / get_moments "
+                         "(IQO/main_parallel.py:202)")
     ap.add_argument("--server-prof", default="", help="run the server under rocprofv3 kernel + HIP trace into DIR")
     args = ap.parse_args()
     if args.serve:
@@ -234,7 +265,10 @@ def main():
             r = fan_out(args, kind, P)
             print(json.dumps(r), flush=True)
             rows.append(r)
-    res = {"n_max": args.n_max, "call": "simulation.step(state, 1/1440, F, 2 pi), F redrawn every 80 steps",
+    ph = physics(args)
+    res = {"family": args.family, "n_max": args.n_max if ph.fock else None, "dim": ph.dim,
+           "call": f"simulation.step(state, 1/{ph.time_steps}, F, gamma) (the driver's defaults), F of the action grid "
+                   f"redrawn every {ph.control_interval} steps",
            "model": "P independent actor processes, one env each (IHO/main_parallel.py:345-359)", "rows": rows}
     if args.out:
         json.dump(res, open(args.out, "w"), indent=1)

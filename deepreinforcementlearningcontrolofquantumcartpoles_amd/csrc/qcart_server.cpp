@@ -112,7 +112,7 @@ struct qc_server {
     double* d_spsi = nullptr;
     bool inplace = false;
     // the resident path: the whole object registered (d_shm), k_resident on its own stream while run() serves
-    bool resident = false, r_running = false;
+    bool resident = false, r_running = false, r_lost = false;   // r_lost: a launch failed, the path is off
     uint8_t* d_shm = nullptr;
     hipStream_t rstream = nullptr;
     hipEvent_t r_exit = nullptr;   // recorded after the resident launch: complete once every wave has exited
@@ -197,9 +197,11 @@ void resident_start(qc_server* s) {
                                           (const uint32_t*)(s->d_shm + ctl), 1.0, s->lease_us * 1e-6, s->r_gen,
                                           s->rstream);
     if (rc != QC_OK || hipEventRecord(s->r_exit, s->rstream) != hipSuccess) {
-        // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0)
+        // no resident kernel: every request goes through the ticks (clients bounce off r_on = 0; a request posted
+        // before they saw it is bounced by resident_tend)
         __atomic_store_n(&H->r_on, 0u, __ATOMIC_SEQ_CST);
         s->resident = false;
+        s->r_lost = true;
         return;
     }
     s->r_running = true;
@@ -209,6 +211,16 @@ void resident_start(qc_server* s) {
 // the server loop's heartbeat (every 100 us at most) and the kernel's state: exited on its own (a heartbeat gap
 // longer than its limit) -> relaunched
 void resident_tend(qc_server* s, double now) {
+    if (s->r_lost) {   // the path was turned off while clients may still post resident requests: they take the ticks
+        for (int e = 0; e < s->P; ++e) {
+            qcs_slot& sl = s->slots[e];
+            const uint32_t rr = __atomic_load_n(&sl.rreq, __ATOMIC_ACQUIRE);
+            if (rr != __atomic_load_n(&sl.rdone, __ATOMIC_ACQUIRE)) {
+                sl.rstatus = QCS_EBOUNCE;
+                __atomic_store_n(&sl.rdone, rr, __ATOMIC_RELEASE);
+            }
+        }
+    }
     if (!s->resident) return;
     if (now - s->t_beat > 100.0) {
         __atomic_store_n(&s->hdr->r_beat, ++s->beat, __ATOMIC_RELAXED);

@@ -339,9 +339,9 @@ int validate_params(const qc_params* p, std::string& err) {
         err = "n_actions must be odd and <= 64";
         return QC_EINVAL;
     }
-    if (p->family >= QC_QO && (p->moment_order < 1 || p->moment_order > kMaxMomentOrder)) {
-        // one observable per lane of the env's wave: (2 + m + 1) m / 2 <= 64
-        err = "moment_order must be in 1..9 (the (2+m+1)*m/2 observables, one per lane of a 64-lane wave)";
+    if (p->family >= QC_QO && (p->moment_order < 1 || p->moment_order > kMaxMomentOrderHi)) {
+        // the observation kernel's instantiations: up to 3 observables per lane of the env's wave
+        err = "moment_order must be in 1..16 (the (2+m+1)*m/2 observables, at most 3 per lane of a 64-lane wave)";
         return QC_EINVAL;
     }
     if (p->a_mode != QC_A_REFERENCE && p->a_mode != QC_A_EXACT) { err = "bad a_mode"; return QC_EINVAL; }

@@ -54,9 +54,12 @@ constexpr uint32_t kNzLds = 1024;
 // HO/simulation.cpp:403-407), kGridBnd points at either end of the grid (QO/simulation_quart.cpp:559-565). The
 // grid step kernel's normalise is specialised on kGridBnd at compile time (qcart_kernels.hpp)
 constexpr int kFockBnd = 5;
-// highest grid moment order (get_moments' MOMENT, QO/setupC.py:16,38): the observation kernel holds observable i in
-// lane i of the env's wave, (2 + m + 1) m / 2 <= 64 (m = 9: 54 observables; m = 10 would need 65)
+// grid moment orders (get_moments' MOMENT, QO/setupC.py:16,38): up to kMaxMomentOrder the observation kernel holds
+// observable i in lane i of the env's wave, (2 + m + 1) m / 2 <= 64 (m = 9: 54 observables); its second instantiation
+// holds observable i in lane i % 64, register i / 64, up to kMaxMomentOrderHi (m = 16: 152 observables, 3 per lane).
+// The step server's shared-object rows hold 64 observables (QCS_MAX_OBS): it serves orders up to kMaxMomentOrder
 constexpr int kMaxMomentOrder = 9;
+constexpr int kMaxMomentOrderHi = 16;
 // the step kernel's fused observation epilogue covers orders up to this one (qc_step runs the observation kernel
 // after the step for higher orders)
 constexpr int kStepMaxMomentOrder = 6;

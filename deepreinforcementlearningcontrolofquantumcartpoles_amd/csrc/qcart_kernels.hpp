@@ -1133,7 +1133,11 @@ __device__ __forceinline__ void grid_p(const cd (&v)[R], cd (&o)[R], double pbar
 // default 5; its p-power passes are unrolled into the step kernel, whose registers the higher orders would cost) —
 // qc_step runs k_obs after the step for orders above it (qcart_api.cpp)
 constexpr int kMaxMoment = kMaxMomentOrder;
+constexpr int kMaxMomentHi = kMaxMomentOrderHi;
 constexpr int kStepMaxMoment = kStepMaxMomentOrder;
+// observables per lane of an order-MM observation vector: 1 while (2 + MM + 1) MM / 2 fits the wave
+template <int MM>
+constexpr int kObsPerLane = ((MM + 3) * MM / 2 + 63) / 64;
 
 // compute_statistics (QO/simulation_quart.cpp:326-362). Returns this lane's entry of the observation vector
 // (lane 0 <x>, lane 1 <p>, lane i >= 2 the centred moment i; lanes >= n_obs: unused): the moments of one p-power b
@@ -1204,6 +1208,72 @@ __device__ __forceinline__ double grid_obs(const cd (&psi)[R], const Coef<2, R>&
     auto ps = [&](int j) -> cd { return psi[j]; };
     grid_obs_pow<MM, 0, R>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
     return ov;
+}
+
+// orders above kMaxMoment (the standalone observation kernel's second instantiation): the same passes with
+// observable i in lane i % 64, register i / 64 (ov[K], K = kObsPerLane<MM>); a copy of grid_obs_pow / grid_obs, so
+// that the step kernels' fused epilogue keeps its code
+template <int MM, int B, int R, int K, typename PS, typename XM>
+__device__ __forceinline__ void grid_obs_pow_k(const PS& ps, const XM& xm, cd (&v)[R], const Coef<2, R>& cf, int lane,
+                                               int m, double xbar, double pbar, double inv_h, double h,
+                                               double (&ov)[K]) {
+    if constexpr (B <= MM) {
+        if (B > m) return;
+        if constexpr (B > 0) {
+            cd nv[R];
+            grid_p<R>(v, nv, pbar, inv_h, cf.N, cf.base, lane);
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = nv[j];
+        }
+        constexpr int A0 = B >= 2 ? 0 : 2 - B, A1 = MM - B, NA = A1 - A0 + 1;
+        double acc[NA];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) acc[i] = 0.0;
+        const auto xs = xm();
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const double xr = xs.x(j) - xbar;
+            const cd pj = ps(j);
+            const double base_re = pj.re * v[j].re + pj.im * v[j].im;   // Re conj(psi) v
+            double xa = 1.0;
+#pragma unroll
+            for (int aa = 0; aa <= A1; ++aa) {
+                if (aa >= A0) acc[aa - A0] += xa * base_re;
+                xa *= xr;
+            }
+        }
+        wave_sum<NA>(acc);
+#pragma unroll
+        for (int aa = A0; aa <= A1; ++aa) {
+            const int jj = aa + B, idx = 2 + (jj - 2) * (jj + 3) / 2 + B;
+            ov[idx >> 6] = lane == (idx & 63) ? acc[aa - A0] * h : ov[idx >> 6];
+        }
+        grid_obs_pow_k<MM, B + 1, R, K>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
+    }
+}
+
+template <int MM, int R, int K, typename XM>
+__device__ __forceinline__ void grid_obs_k(const cd (&psi)[R], const Coef<2, R>& cf, const XM& xm, int lane, int m,
+                                           double h, double (&ov)[K]) {
+    const double inv_h = 1.0 / h;
+    cd v[R];
+    double s2[2] = {0, 0};
+    grid_p<R>(psi, v, 0.0, inv_h, cf.N, cf.base, lane);
+    const auto xs = xm();
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        s2[0] += xs.x(j) * (psi[j].re * psi[j].re + psi[j].im * psi[j].im);
+        s2[1] += psi[j].re * v[j].re + psi[j].im * v[j].im;
+    }
+    wave_sum<2>(s2);
+    const double xbar = s2[0] * h, pbar = s2[1] * h;
+    ov[0] = lane == 0 ? xbar : pbar;
+#pragma unroll
+    for (int k = 1; k < K; ++k) ov[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = psi[j];
+    auto ps = [&](int j) -> cd { return psi[j]; };
+    grid_obs_pow_k<MM, 0, R, K>(ps, xm, v, cf, lane, m, xbar, pbar, inv_h, h, ov);
 }
 
 // ---- the fused multi-step kernel ------------------------------------------------------------
@@ -2491,7 +2561,7 @@ __device__ __forceinline__ cd ld_psi(const void* p, size_t i) {
     const RT* q = (const RT*)p;
     return C((double)q[2 * i], (double)q[2 * i + 1]);
 }
-template <int FAM, int R, typename RT = double>
+template <int FAM, int R, typename RT = double, int MM = kMaxMoment>
 __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t env = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -2514,8 +2584,17 @@ __global__ __launch_bounds__(256) void k_obs(const KArgs a) {
         }
     } else {
         auto xm = [&]() { return RowReg<R>{cf.xg, cf.xg}; };
-        const double v = grid_obs<kMaxMoment, R>(psi, cf, xm, lane, a.moment_order, a.h);
-        if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
+        if constexpr (MM <= kMaxMoment) {
+            const double v = grid_obs<MM, R>(psi, cf, xm, lane, a.moment_order, a.h);
+            if (lane < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane] = v;
+        } else {
+            constexpr int K = kObsPerLane<MM>;
+            double v[K];
+            grid_obs_k<MM, R, K>(psi, cf, xm, lane, a.moment_order, a.h, v);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (lane + 64 * k < a.n_obs) a.obs_out[(size_t)env * a.n_obs + lane + 64 * k] = v[k];
+        }
     }
 }
 
@@ -2844,7 +2923,15 @@ int launch_one(int kind, const KArgs& a, int what, double xth, void* out, int rk
                              : launch_step_mode<FAM, R, 0, RT>(a, st);
         if (rc) return rc;
     }
-    else if (kind == 1) hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);
+    else if (kind == 1) {
+        // orders above kMaxMoment (grid): the instantiation with several observables per lane
+        if constexpr (FAM == 2) {
+            if (a.moment_order > kMaxMoment) hipLaunchKernelGGL((k_obs<FAM, R, RT, kMaxMomentHi>), grid, block, 0, st, a);
+            else hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);
+        } else {
+            hipLaunchKernelGGL((k_obs<FAM, R, RT>), grid, block, 0, st, a);
+        }
+    }
     else if (kind == 2) hipLaunchKernelGGL((k_aux<FAM, R, RT>), grid, block, 0, st, a, what, xth, out);
     else if (kind == 5) hipLaunchKernelGGL((k_control<FAM, R, RT>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_reset<FAM, R, RT>), grid, block, 0, st, a, rkind, mask, a0, a1, a2, k_arr, m_arr, s_arr);

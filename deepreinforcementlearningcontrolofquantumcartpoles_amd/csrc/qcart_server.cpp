@@ -517,6 +517,8 @@ int qc_server_create(const qc_params* p, int device, int32_t max_clients, const 
         delete s;
         return code;
     };
+    if (s->n_obs > QCS_MAX_OBS)   // the shared object's observation rows (grid moment orders <= 9)
+        return bail(QC_EINVAL, "the step server serves moment_order <= 9 (its observation rows hold 64 values)");
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(QC_EHIP, "hipStreamCreate failed");
     if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess)

@@ -65,10 +65,11 @@ typedef struct qc_params {
     double grid_size;      /* grid: GRID_SIZE (h)                                                */
     double lambda_;        /* grid: LAMBDA (already multiplied by pi, IQO/main_parallel.py:29)  */
     double mass;           /* grid: MASS (already divided by pi)                                 */
-    int32_t moment_order;  /* grid: MOMENT macro (default 5 -> 20 observables); 1..9: one       */
-                           /* observable per lane of the env's 64-lane wave, (2+m+1)m/2 <= 64 */
-                           /* (QO/setupC.py:16,38 compiles any m >= 1; m >= 10 is refused,    */
-                           /* QC_EINVAL)                                                      */
+    int32_t moment_order;  /* grid: MOMENT macro (default 5 -> 20 observables); 1..16: up to 9 */
+                           /* one observable per lane of the env's 64-lane wave, above that   */
+                           /* up to 3 per lane ((2+m+1)m/2 <= 152) (QO/setupC.py:16,38        */
+                           /* compiles any m >= 1; m >= 17 is refused, QC_EINVAL; the step    */
+                           /* server serves m <= 9)                                           */
     int32_t a_mode;        /* enum qc_a_mode                                                     */
     double gamma;          /* measurement strength (step() argument; the drivers pass args.gamma*pi) */
     double dt;             /* time step (step() argument; 1/time_steps)                         */

@@ -70,16 +70,16 @@ def test_params_struct_matches_header(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libqcart.so not built")
 def test_moment_order_range_is_validated_before_the_device():
-    """get_moments orders 1..9 (one observable per lane, (2+m+1)m/2 <= 64); 10 is refused with the reason,
+    """get_moments orders 1..16 (at most 3 observables per lane of the env's wave); 17 is refused with the reason,
     before any device is touched (QO/setupC.py compiles any MOMENT >= 1)."""
     from deepreinforcementlearningcontrolofquantumcartpoles_amd import _lib
     p = _lib.QcParams()
     p.family, p.x_max, p.grid_size, p.lambda_, p.mass = 2, 8.5, 0.1, 0.04 * 3.14159, 1 / 3.14159
-    p.gamma, p.dt, p.f_max, p.n_actions, p.batch, p.moment_order = 0.0314, 1 / 1440, 5.0, 21, 2, 10
+    p.gamma, p.dt, p.f_max, p.n_actions, p.batch, p.moment_order = 0.0314, 1 / 1440, 5.0, 21, 2, 17
     h = ctypes.c_void_p()
     rc = _lib.lib().qc_create(ctypes.byref(p), 0, ctypes.byref(h))
     assert rc == -1 and not h.value
-    assert b"1..9" in _lib.lib().qc_last_error(None)
+    assert b"1..16" in _lib.lib().qc_last_error(None)
 
 
 CLIENT = os.path.join(ROOT, "deepreinforcementlearningcontrolofquantumcartpoles_amd", "libqcart_client.so")

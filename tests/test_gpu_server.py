@@ -407,6 +407,9 @@ def test_served_errors():
         srv.close()
     with pytest.raises(RuntimeError, match="no step server"):
         S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=63), name)
+    # grid moment orders above 9 (65+ observables) are the in-process module's: the server's rows hold 64
+    with pytest.raises(Exception, match="moment_order <= 9"):
+        S.StepServer(cfg.QO, max_clients=1, name=_name(), moment_order=10)
 
 
 def test_killed_client_slot_is_released():

@@ -81,7 +81,7 @@ class MockServer:
     minus the sum of Re(psi); the observation row 100, 101, ...), bouncing action `bounce` and steps of another
     dynamics generation than r_gen to the ticks."""
 
-    def __init__(self, name, P=3, N=8, n_obs=5, serve_ops=None, resident=False, bounce=-1):
+    def __init__(self, name, P=3, N=8, n_obs=5, serve_ops=None, resident=False, bounce=-1, grid_kernel=False):
         self.name, self.P, self.N, self.n_obs = name, P, N, n_obs
         self.serve_ops = serve_ops
         rnd = lambda v: (v + 4095) // 4096 * 4096   # noqa: E731
@@ -102,6 +102,7 @@ class MockServer:
         h.magic, h.version, h.max_clients, h.N, h.n_obs, h.family = 0x56534351, VERSION, P, N, n_obs, 1
         h.f_max, h.n_actions = 8.0, 21
         self.bounce = bounce
+        self.grid_kernel = grid_kernel   # a grid family's resident kernel: every non-step op bounces (the reset too)
         self.kernel_gen = None   # the "kernel's" generation (None: the header's)
         if resident:
             h.r_on, h.r_dt, h.r_gamma = 1, 1 / 1440, 6.28
@@ -125,7 +126,9 @@ class MockServer:
                     _, op, act, gen, _, _ = rq_fields(s.rreq)
                     kgen = self.hdr.r_gen if self.kernel_gen is None else self.kernel_gen
                     if op == 3:
-                        s.rstatus = 0
+                        s.rstatus = EBOUNCE if self.grid_kernel else 0
+                    elif op != 0 and self.grid_kernel:
+                        s.rstatus = EBOUNCE
                     elif op == 1:
                         s.value, s.rstatus = -float(self.psi[e].real.sum()), 0
                     elif op == 2:
@@ -302,6 +305,26 @@ def test_client_takes_the_resident_path():
         t0 = time.monotonic()
         a.close()
         assert time.monotonic() - t0 < 1.0 and srv.hdr.n_clients == 0
+    finally:
+        srv.close()
+
+
+def test_client_opens_on_a_grid_resident_kernel():
+    """A grid family's resident kernel answers the reset a new owner sends at open with a bounce (every non-step op
+    bounces there): the module still opens, and its steps take the resident path."""
+    S = _client_module()
+    from deepreinforcementlearningcontrolofquantumcartpoles_amd import config as cfg
+    srv = MockServer(f"/qcart_mockg_{os.getpid()}", P=1, N=8, resident=True, grid_kernel=True)
+    try:
+        a = S._ServedSimulation(cfg.DEFAULTS[cfg.IHO].with_(n_max=7, omega=3.14159), srv.name)
+        s0 = srv.slots[0]
+        assert rq_fields(s0.rreq)[1] == 3 and s0.rstatus == EBOUNCE and s0.rcount == 1
+        base = (np.arange(8) + 1j).astype(np.complex128)
+        st = base.copy()
+        q, xm, fail = a.step(st, 1 / 1440, 0.8, 6.28)
+        assert q == 111.0 and np.array_equal(st, 3 * base) and s0.rcount == 2
+        del s0
+        a.close()
     finally:
         srv.close()
 
